@@ -1,0 +1,57 @@
+// Bitsliced layout helpers (device): 32x32 bit transposes in registers and the
+// BitsliceUtils<128> block mapping of the reference (src/ulvt/utils/bitslicing.cuh:32-64):
+// compact element e, limb l (word 4e+l of a 128-word block) <-> word 32l+i, bit e.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bitsliced_gen.hpp"
+
+namespace bn {
+
+// In-place 32x32 bit transpose (recursive block swap): afterwards bit j of word i is
+// bit i of word j of the input. Fully unrolled: all indices are compile-time constants.
+__device__ __forceinline__ void transpose32(uint32_t* a) {
+#pragma unroll
+	for (int lj = 4; lj >= 0; lj--) {
+		const int j = 1 << lj;
+		const uint32_t m = lj == 4 ? 0x0000FFFFu
+						 : lj == 3 ? 0x00FF00FFu
+						 : lj == 2 ? 0x0F0F0F0Fu
+						 : lj == 1 ? 0x33333333u
+								   : 0x55555555u;
+#pragma unroll
+		for (int k = 0; k < 32; k++) {
+			if (k & j) continue;
+			const uint32_t t = ((a[k] >> j) ^ a[k + j]) & m;
+			a[k] ^= t << j;
+			a[k + j] ^= t;
+		}
+	}
+}
+
+__device__ __forceinline__ void bs_transpose128(uint32_t* r) {
+	uint32_t t[128];
+#pragma unroll
+	for (int i = 0; i < 128; i++) t[32 * (i & 3) + (i >> 2)] = r[i];
+#pragma unroll
+	for (int c = 0; c < 4; c++) transpose32(t + 32 * c);
+#pragma unroll
+	for (int i = 0; i < 128; i++) r[i] = t[i];
+}
+
+__device__ __forceinline__ void bs_untranspose128(uint32_t* r) {
+	uint32_t t[128];
+#pragma unroll
+	for (int i = 0; i < 128; i++) t[i] = r[i];
+#pragma unroll
+	for (int c = 0; c < 4; c++) transpose32(t + 32 * c);
+#pragma unroll
+	for (int i = 0; i < 128; i++) r[4 * (i & 31) + (i >> 5)] = t[i];
+}
+
+// 32 GF(2^128) products on bitsliced blocks (multiply_unrolled<7> semantics), alias-safe.
+__device__ __forceinline__ void bs_mul128(const uint32_t* a, const uint32_t* b, uint32_t* out) { bsm7_mul(a, b, out); }
+
+}  // namespace bn

@@ -1,0 +1,139 @@
+// Tower-field kernels behind the C-ABI: elementwise compact GF(2^32)/GF(2^128) products,
+// compact <-> bitsliced conversion, bitsliced GF(2^128) products and the register-resident
+// repeat-loop microbenchmarks (config 2).
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+#include "field_dev.hpp"
+#include "bitsliced.hpp"
+
+namespace bn {
+
+__global__ void k_gf32_mul(const uint32_t* a, const uint32_t* b, uint32_t* o, size_t n) {
+	for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+		o[i] = dmul<5>(a[i], b[i]);
+}
+
+__global__ void k_gf128_mul(const uint4* a, const uint4* b, uint4* o, size_t n) {
+	for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+		o[i] = dmul128(a[i], b[i]);
+}
+
+// One thread per 128-word block (transpose_kernel / untranspose_kernel,
+// src/ulvt/utils/bitslicing.cuh:89-105), 32x32 transposes in registers.
+__global__ __launch_bounds__(256) void k_bitslice(uint32_t* buf, size_t nblk, int untranspose) {
+	for (size_t b = blockIdx.x * (size_t)blockDim.x + threadIdx.x; b < nblk; b += (size_t)gridDim.x * blockDim.x) {
+		uint32_t* p = buf + 128 * b;
+		uint32_t r[128];
+#pragma unroll
+		for (int i = 0; i < 128; i++) r[i] = p[i];
+		if (!untranspose)
+			bs_transpose128(r);
+		else
+			bs_untranspose128(r);
+#pragma unroll
+		for (int i = 0; i < 128; i++) p[i] = r[i];
+	}
+}
+
+__global__ __launch_bounds__(256) void k_gf128_mul_bs(const uint32_t* a, const uint32_t* b, uint32_t* o, size_t nblk) {
+	for (size_t blk = blockIdx.x * (size_t)blockDim.x + threadIdx.x; blk < nblk; blk += (size_t)gridDim.x * blockDim.x) {
+		uint32_t x[128], y[128], z[128];
+#pragma unroll
+		for (int i = 0; i < 128; i++) {
+			x[i] = a[128 * blk + i];
+			y[i] = b[128 * blk + i];
+		}
+		bs_mul128(x, y, z);
+#pragma unroll
+		for (int i = 0; i < 128; i++) o[128 * blk + i] = z[i];
+	}
+}
+
+// bitsliced_repeat-style microbenchmarks (src/ulvt/finite_fields/tests/profiling/kernels/
+// bitsliced_repeat.cu:5-32): `iters` dependent products per lane, operands register-resident.
+__global__ __launch_bounds__(256) void k_repeat_compact(uint4* state, const uint4* operand, size_t threads, int iters) {
+	const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+	if (t >= threads) return;
+	uint4 x = state[t];
+	const uint4 y = operand[t];
+	for (int i = 0; i < iters; i++) x = dmul128(x, y);
+	state[t] = x;
+}
+
+__global__ __launch_bounds__(256) void k_repeat_bitsliced(uint32_t* state, const uint32_t* operand, size_t threads, int iters) {
+	const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+	if (t >= threads) return;
+	uint32_t x[128], y[128];
+#pragma unroll
+	for (int i = 0; i < 128; i++) {
+		x[i] = state[128 * t + i];
+		y[i] = operand[128 * t + i];
+	}
+	for (int it = 0; it < iters; it++) bs_mul128(x, y, x);
+#pragma unroll
+	for (int i = 0; i < 128; i++) state[128 * t + i] = x[i];
+}
+
+static unsigned grid_for(size_t n, unsigned block) {
+	size_t g = (n + block - 1) / block;
+	if (g > 65535u * 16u) g = 65535u * 16u;
+	return (unsigned)(g ? g : 1);
+}
+
+}  // namespace bn
+
+using namespace bn;
+
+extern "C" int bn_gf32_mul_device(const void* a, const void* b, void* o, size_t n, void* stream) {
+	BN_CHECK_ARG(a && b && o, "NULL device pointer");
+	if (!n) return BN_OK;
+	hipLaunchKernelGGL(k_gf32_mul, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, (const uint32_t*)a,
+					   (const uint32_t*)b, (uint32_t*)o, n);
+	BN_HIP(hipGetLastError());
+	return BN_OK;
+}
+
+extern "C" int bn_gf128_mul_device(const void* a, const void* b, void* o, size_t n, void* stream) {
+	BN_CHECK_ARG(a && b && o, "NULL device pointer");
+	if (!n) return BN_OK;
+	hipLaunchKernelGGL(k_gf128_mul, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, (const uint4*)a,
+					   (const uint4*)b, (uint4*)o, n);
+	BN_HIP(hipGetLastError());
+	return BN_OK;
+}
+
+extern "C" int bn_bitslice_device(void* buf, size_t nblk, int untranspose, void* stream) {
+	BN_CHECK_ARG(buf, "NULL device pointer");
+	if (!nblk) return BN_OK;
+	hipLaunchKernelGGL(k_bitslice, dim3(grid_for(nblk, 256)), dim3(256), 0, (hipStream_t)stream, (uint32_t*)buf, nblk,
+					   untranspose);
+	BN_HIP(hipGetLastError());
+	return BN_OK;
+}
+
+extern "C" int bn_gf128_mul_bitsliced_device(const void* a, const void* b, void* o, size_t nblk, void* stream) {
+	BN_CHECK_ARG(a && b && o, "NULL device pointer");
+	if (!nblk) return BN_OK;
+	hipLaunchKernelGGL(k_gf128_mul_bs, dim3(grid_for(nblk, 256)), dim3(256), 0, (hipStream_t)stream,
+					   (const uint32_t*)a, (const uint32_t*)b, (uint32_t*)o, nblk);
+	BN_HIP(hipGetLastError());
+	return BN_OK;
+}
+
+extern "C" int bn_gf128_mul_repeat_device(int kind, void* state, const void* operand, size_t threads, int iters,
+										  void* stream) {
+	BN_CHECK_ARG(state && operand, "NULL device pointer");
+	BN_CHECK_ARG(kind == 0 || kind == 1, "kind must be 0 (compact) or 1 (bitsliced)");
+	BN_CHECK_ARG(iters >= 0, "iters must be >= 0");
+	if (!threads) return BN_OK;
+	const unsigned grid = (unsigned)((threads + 255) / 256);
+	if (kind == 0)
+		hipLaunchKernelGGL(k_repeat_compact, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint4*)state,
+						   (const uint4*)operand, threads, iters);
+	else
+		hipLaunchKernelGGL(k_repeat_bitsliced, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint32_t*)state,
+						   (const uint32_t*)operand, threads, iters);
+	BN_HIP(hipGetLastError());
+	return BN_OK;
+}

@@ -1,0 +1,63 @@
+// Binary tower field GF(2^(2^h)) in compact form, host + device.
+//
+// Tower (Fan-Paar / Wiedemann, as src/ulvt/finite_fields/binary_tower.cuh:19-128):
+//   level 0 = GF(2); level h = level(h-1)[X_{h-1}] / (X^2 + alpha_{h-1} X + 1),
+//   alpha_0 = 1, alpha_h = X_{h-1}. An element of level h is 2^h bits: low half = the
+//   level-(h-1) coefficient of 1, high half = the coefficient of X_{h-1}.
+// Used on the host for twiddle precomputation and on the device by the v0 kernels,
+// the compact GF(2^128) multiply and the sumcheck verifier helpers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bn {
+
+// multiply by alpha of level h (i.e. by X_{h-1}); (a0 + a1 X)X = a1 + (a0 + a1 alpha_{h-1}) X
+__host__ __device__ constexpr uint64_t tw_mul_alpha(uint64_t a, int h) {
+	if (h == 0) return a & 1;
+	const int half = 1 << (h - 1);
+	const uint64_t m = half >= 64 ? ~0ull : ((1ull << half) - 1);
+	const uint64_t a0 = a & m, a1 = (a >> half) & m;
+	return a1 | ((a0 ^ tw_mul_alpha(a1, h - 1)) << half);
+}
+
+// Karatsuba recursion to GF(2).
+__host__ __device__ constexpr uint64_t tw_mul(uint64_t a, uint64_t b, int h) {
+	if (h == 0) return a & b & 1;
+	const int half = 1 << (h - 1);
+	const uint64_t m = half >= 64 ? ~0ull : ((1ull << half) - 1);
+	const uint64_t a0 = a & m, a1 = (a >> half) & m, b0 = b & m, b1 = (b >> half) & m;
+	const uint64_t z0 = tw_mul(a0, b0, h - 1);
+	const uint64_t z2 = tw_mul(a1, b1, h - 1);
+	const uint64_t z1 = tw_mul(a0 ^ a1, b0 ^ b1, h - 1) ^ z0 ^ z2;
+	return (z0 ^ z2) | ((z1 ^ tw_mul_alpha(z2, h - 1)) << half);
+}
+
+__host__ __device__ constexpr uint64_t tw_square(uint64_t a, int h) { return tw_mul(a, a, h); }
+
+__host__ __device__ constexpr uint64_t tw_inv(uint64_t a, int h) {
+	if (h == 0) return a & 1;
+	const int half = 1 << (h - 1);
+	const uint64_t m = half >= 64 ? ~0ull : ((1ull << half) - 1);
+	if ((a >> half) == 0) return tw_inv(a, h - 1);
+	const uint64_t a0 = a & m, a1 = (a >> half) & m;
+	const uint64_t inter = a0 ^ tw_mul_alpha(a1, h - 1);
+	const uint64_t delta = tw_mul(a0, inter, h - 1) ^ tw_square(a1, h - 1);
+	const uint64_t dinv = tw_inv(delta, h - 1);
+	return tw_mul(dinv, inter, h - 1) | (tw_mul(dinv, a1, h - 1) << half);
+}
+
+// GF(2^128) as (lo, hi) u64 pair; schoolbook top level like tower_height_7_mul
+// (src/ulvt/sumcheck/test/utils/tower_7_mul.cu:4-20), Karatsuba below.
+struct u128p {
+	uint64_t lo, hi;
+};
+__host__ __device__ inline u128p tw_mul128(u128p a, u128p b) {
+	const uint64_t z0 = tw_mul(a.lo, b.lo, 6);
+	const uint64_t z2 = tw_mul(a.hi, b.hi, 6);
+	const uint64_t z1 = tw_mul(a.lo ^ a.hi, b.lo ^ b.hi, 6) ^ z0 ^ z2;
+	return u128p{z0 ^ z2, z1 ^ tw_mul_alpha(z2, 6)};
+}
+
+}  // namespace bn

@@ -1,0 +1,291 @@
+"""Python mirror of the reference's ulvt_gpu / sumcheck library surface over the C-ABI.
+
+The product is the C-ABI shared library (binius-ntt_amd/lib/libbinius_ntt_amd.so, declared in
+include/binius_ntt_amd.h); this module binds it with ctypes and mirrors the reference's C++
+classes so parity tests read like the reference's own:
+
+  NTTData, DataOrder                  src/ulvt/ntt/nttconf.cuh:9-21
+  AdditiveNTTConf(log_h, log_rate)    src/ulvt/ntt/nttconf.cuh:49-60
+  AdditiveNTT(conf).apply(in, out)    src/ulvt/ntt/additive_ntt.cuh:175-265
+  Sumcheck(num_vars, d, transposed)   src/ulvt/sumcheck/sumcheck.cuh:10-301
+  check_gpu_capabilities()            src/ulvt/utils/common.cu:6-43
+
+Device buffers are torch tensors (PyTorch-ROCm is only plumbing here: memory, streams,
+torch.distributed). There is no CPU fallback: if the library is missing every call raises.
+"""
+import ctypes
+import enum
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(os.path.dirname(_HERE))  # binius-ntt_amd/
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libbinius_ntt_amd.so")
+HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "binius_ntt_amd.h")
+
+BN_OK, BN_ERR_INVALID, BN_ERR_HIP, BN_ERR_UNSUPPORTED, BN_ERR_ALLOC = 0, 1, 2, 3, 4
+_ERRNAMES = {1: "BN_ERR_INVALID", 2: "BN_ERR_HIP", 3: "BN_ERR_UNSUPPORTED", 4: "BN_ERR_ALLOC"}
+
+_lib = None
+
+
+class BnError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s: %s" % (_ERRNAMES.get(code, code), msg))
+        self.code = code
+
+
+def lib():
+    """Load the HIP engine. Raises if it has not been built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libbinius_ntt_amd.so not built (run `make -C binius-ntt_amd` or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, i32, u32p = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)
+    sig = {
+        "bn_last_error": (ctypes.c_char_p, []),
+        "bn_version": (ctypes.c_char_p, []),
+        "bn_check_gpu_capabilities": (i32, []),
+        "bn_antt_plan_create": (i32, [i32, i32, i32, i32, ctypes.POINTER(vp)]),
+        "bn_antt_plan_destroy": (i32, [vp]),
+        "bn_antt_forward_host": (i32, [vp, vp, sz, vp]),
+        "bn_antt_forward_device": (i32, [vp, vp, vp, sz, vp]),
+        "bn_antt_get_subspace_evals": (i32, [vp, u32p, sz]),
+        "bn_antt_plan_query": (i32, [vp, i32, ctypes.POINTER(ctypes.c_int64)]),
+        "bn_antt_set_event_timing": (i32, [vp, i32]),
+        "bn_antt_get_event_timing": (i32, [vp, ctypes.POINTER(ctypes.c_float), i32, ctypes.POINTER(i32)]),
+        "bn_gf128_mul_device": (i32, [vp, vp, vp, sz, vp]),
+        "bn_gf128_mul_bitsliced_device": (i32, [vp, vp, vp, sz, vp]),
+        "bn_gf32_mul_device": (i32, [vp, vp, vp, sz, vp]),
+        "bn_gf128_mul_repeat_device": (i32, [i32, vp, vp, sz, i32, vp]),
+        "bn_bitslice_device": (i32, [vp, sz, i32, vp]),
+        "bn_sumcheck_create": (i32, [i32, i32, i32, i32, u32p, ctypes.POINTER(vp)]),
+        "bn_sumcheck_create_device": (i32, [i32, i32, i32, i32, vp, i32, ctypes.POINTER(vp)]),
+        "bn_sumcheck_round_messages": (i32, [vp, u32p, u32p]),
+        "bn_sumcheck_move_to_next_round": (i32, [vp, u32p]),
+        "bn_sumcheck_round": (i32, [vp, ctypes.POINTER(i32)]),
+        "bn_sumcheck_set_shard": (i32, [vp, i32, i32]),
+        "bn_sumcheck_destroy": (i32, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != BN_OK:
+        raise BnError(rc, lib().bn_last_error().decode())
+
+
+def exported_symbols():
+    """Names declared in include/binius_ntt_amd.h (used by the ABI test)."""
+    import re
+    with open(HEADER_PATH) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(bn_\w+)\s*\(", src, re.M)))
+
+
+def check_gpu_capabilities():
+    return bool(lib().bn_check_gpu_capabilities())
+
+
+def _ptr(t):
+    """Device pointer of a torch tensor (or an int address)."""
+    if isinstance(t, int):
+        return ctypes.c_void_p(t)
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(stream):
+    if stream is None:
+        import torch
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if isinstance(stream, int):
+        return ctypes.c_void_p(stream)
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+# ------------------------------------------------------------------ NTT data / config
+class DataOrder(enum.IntEnum):
+    """nttconf.cuh:9"""
+    INVALID = -1
+    IN_ORDER = 0
+    BIT_REVERSED = 1
+
+
+class NTTData:
+    """Host-owned buffer (nttconf.cuh:11-21). `data` is a numpy array of `size` elements:
+    uint32 for GF(2^32), shape (size, 4) uint32 limbs for GF(2^128)."""
+
+    def __init__(self, size, order=DataOrder.INVALID, field_bits=32, data=None):
+        self.order = DataOrder(order)
+        self.size = int(size)
+        self.field_bits = field_bits
+        if data is not None:
+            self.data = np.ascontiguousarray(data, dtype=np.uint32)
+        elif field_bits == 32:
+            self.data = np.zeros(self.size, np.uint32)
+        else:
+            self.data = np.zeros((self.size, field_bits // 32), np.uint32)
+
+    def byte_len(self):
+        return self.data.nbytes
+
+
+class FanPaarTowerField:
+    """Field policy tag (binary_tower.cuh:111-128): height 5 = GF(2^32), height 7 = GF(2^128)."""
+
+    def __init__(self, height):
+        assert height in (5, 7), "the NTT is built for GF(2^32) and GF(2^128)"
+        self.height = height
+
+    def N_BITS(self):
+        return 1 << self.height
+
+
+class AdditiveNTTConf:
+    """nttconf.cuh:49-60; the reference ASSERTs (aborts) on bad parameters, this raises."""
+
+    def __init__(self, log_h, log_rate, field=FanPaarTowerField(5), device=0):
+        if not log_h >= 1:
+            raise ValueError("log_h must be >= 1")
+        if not (0 <= log_rate <= 4):
+            raise ValueError("log_rate must be in [0, 4]")
+        if not log_h + log_rate <= field.N_BITS():
+            raise ValueError("log_h + log_rate must be <= N_BITS")
+        self.log_h, self.log_rate, self.field, self.device = log_h, log_rate, field, device
+
+
+class AdditiveNTT:
+    """additive_ntt.cuh:175-319 over the C-ABI plan."""
+
+    def __init__(self, conf):
+        self.conf = conf
+        self.field_bits = conf.field.N_BITS()
+        p = ctypes.c_void_p()
+        _check(lib().bn_antt_plan_create(conf.device, self.field_bits, conf.log_h, conf.log_rate, ctypes.byref(p)))
+        self._plan = p
+
+    def close(self):
+        if getattr(self, "_plan", None) is not None and self._plan.value:
+            lib().bn_antt_plan_destroy(self._plan)
+            self._plan = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def limbs(self):
+        return self.field_bits // 32
+
+    def apply(self, inp, out):
+        """Reference semantics (additive_ntt.cuh:201-265): False (no other effect) unless
+        inp.size == 2^log_h and inp.order == IN_ORDER; fills out (coset-major) synchronously."""
+        n = 1 << self.conf.log_h
+        if inp.size != n or inp.order != DataOrder.IN_ORDER:
+            return False
+        src = np.ascontiguousarray(inp.data, dtype=np.uint32)
+        assert src.size == n * self.limbs
+        n_out = n << self.conf.log_rate
+        if out.data.size != n_out * self.limbs:
+            out.data = np.zeros((n_out,) if self.limbs == 1 else (n_out, self.limbs), np.uint32)
+            out.size = n_out
+        dst = out.data
+        _check(lib().bn_antt_forward_host(self._plan, src.ctypes.data, n, dst.ctypes.data))
+        out.order = DataOrder.IN_ORDER
+        return True
+
+    def forward_device(self, d_in, d_out, batch=1, stream=None):
+        """Device-resident transform(s) on torch tensors (or raw addresses); async on `stream`."""
+        _check(lib().bn_antt_forward_device(self._plan, _ptr(d_in), _ptr(d_out), batch, _stream(stream)))
+
+    def subspace_evals(self):
+        lh, w = self.conf.log_h, self.conf.log_h + self.conf.log_rate - 1
+        out = np.zeros(max(1, lh * w), np.uint32)
+        _check(lib().bn_antt_get_subspace_evals(self._plan, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), out.size))
+        return out[: lh * w].reshape(lh, w)
+
+    def variant(self):
+        v = ctypes.c_int64()
+        _check(lib().bn_antt_plan_query(self._plan, 4, ctypes.byref(v)))
+        return v.value
+
+    def set_event_timing(self, enable):
+        _check(lib().bn_antt_set_event_timing(self._plan, 1 if enable else 0))
+
+    def event_timing(self):
+        arr = (ctypes.c_float * 16)()
+        n = ctypes.c_int()
+        _check(lib().bn_antt_get_event_timing(self._plan, arr, 16, ctypes.byref(n)))
+        return [arr[i] for i in range(min(n.value, 16))]
+
+
+# ------------------------------------------------------------------ field / bitslicing
+def gf128_mul(a, b, out, stream=None):
+    _check(lib().bn_gf128_mul_device(_ptr(a), _ptr(b), _ptr(out), a.numel() // 4, _stream(stream)))
+
+
+def gf32_mul(a, b, out, stream=None):
+    _check(lib().bn_gf32_mul_device(_ptr(a), _ptr(b), _ptr(out), a.numel(), _stream(stream)))
+
+
+def gf128_mul_bitsliced(a, b, out, stream=None):
+    _check(lib().bn_gf128_mul_bitsliced_device(_ptr(a), _ptr(b), _ptr(out), a.numel() // 128, _stream(stream)))
+
+
+def gf128_mul_repeat(kind, state, operand, threads, iters, stream=None):
+    _check(lib().bn_gf128_mul_repeat_device(kind, _ptr(state), _ptr(operand), threads, iters, _stream(stream)))
+
+
+def bitslice(buf, untranspose=False, stream=None):
+    _check(lib().bn_bitslice_device(_ptr(buf), buf.numel() // 128, 1 if untranspose else 0, _stream(stream)))
+
+
+# ------------------------------------------------------------------ sumcheck
+class Sumcheck:
+    """Sumcheck<NUM_VARS, COMPOSITION_SIZE, DATA_IS_TRANSPOSED> (sumcheck.cuh:10-301)."""
+
+    def __init__(self, num_vars, composition_size, data_is_transposed, evals, device=0, shard=None):
+        self.num_vars, self.d = num_vars, composition_size
+        p = ctypes.c_void_p()
+        if isinstance(evals, np.ndarray):
+            ev = np.ascontiguousarray(evals, dtype=np.uint32).reshape(-1)
+            _check(lib().bn_sumcheck_create(device, num_vars, composition_size, 1 if data_is_transposed else 0,
+                                            ev.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(p)))
+        else:
+            _check(lib().bn_sumcheck_create_device(device, num_vars, composition_size,
+                                                   1 if data_is_transposed else 0, _ptr(evals), 0, ctypes.byref(p)))
+        self._sc = p
+        if shard is not None:
+            _check(lib().bn_sumcheck_set_shard(self._sc, shard[0], shard[1]))
+
+    def this_round_messages(self):
+        s = np.zeros(4, np.uint32)
+        pts = np.zeros(4 * (self.d + 1), np.uint32)
+        _check(lib().bn_sumcheck_round_messages(self._sc, s.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                                pts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))))
+        return s, pts.reshape(self.d + 1, 4)
+
+    def move_to_next_round(self, challenge):
+        c = np.ascontiguousarray(challenge, dtype=np.uint32).reshape(4)
+        _check(lib().bn_sumcheck_move_to_next_round(self._sc, c.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))))
+
+    def close(self):
+        if getattr(self, "_sc", None) is not None and self._sc.value:
+            lib().bn_sumcheck_destroy(self._sc)
+            self._sc = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

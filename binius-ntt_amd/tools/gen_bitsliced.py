@@ -1,0 +1,277 @@
+#!/usr/bin/env python3
+"""Bitsliced binary-tower multiplier generator (gfx950 flavour).
+
+MI355X-native successor of the reference's circuit generator
+(src/ulvt/finite_fields/circuit_generator/multiply_and_generate_circuit.cpp:86-241, which
+symbolically executes the recursive Karatsuba tower multiply and prints one C statement per
+gate). Differences that matter on CDNA4:
+
+* gates are hash-consed (common subexpressions are computed once);
+* XOR chains and AND->XOR pairs are fused into gfx950's 3-input v_bitop3_b32
+  (XOR3 = 0x96, (a&b)^c = 0x6a) through __builtin_amdgcn_bitop3_b32 — hipcc does not form
+  XOR3 on its own;
+* the multiplier is split into prep(w) (the w-side Karatsuba operand sums, computed once
+  per twiddle and reused across many words) and mulp(x, prep(w)).
+
+Word i of a bitsliced operand holds bit i (tower basis) of 32 independent field elements.
+Output: binius-ntt_amd/csrc/bitsliced_gen.hpp
+"""
+import os
+import sys
+
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "bitsliced_gen.hpp")
+
+
+class DAG:
+    def __init__(self):
+        self.nodes = []  # (op, args)  op in {'in','and','xor'}
+        self.index = {}
+
+    def node(self, op, args):
+        if op == "xor":
+            args = tuple(sorted(args))
+        elif op == "and":
+            args = tuple(sorted(args))
+        key = (op, args)
+        if key in self.index:
+            return self.index[key]
+        self.nodes.append(key)
+        self.index[key] = len(self.nodes) - 1
+        return len(self.nodes) - 1
+
+    def inp(self, name):
+        return self.node("in", (name,))
+
+    def xor(self, a, b):
+        if a is None:
+            return b
+        if b is None:
+            return a
+        if a == b:
+            return None  # zero
+        return self.node("xor", (a, b))
+
+    def and_(self, a, b):
+        if a is None or b is None:
+            return None
+        return self.node("and", (a, b))
+
+
+def vadd(d, a, b):
+    return [d.xor(x, y) for x, y in zip(a, b)]
+
+
+def mul_alpha(d, a, h):
+    """(a0 + a1 X)X = a1 + (a0 + a1 alpha_{h-1}) X   (binary_tower.cuh:83-93)."""
+    if h == 0:
+        return list(a)
+    half = 1 << (h - 1)
+    a0, a1 = a[:half], a[half:]
+    return a1 + vadd(d, a0, mul_alpha(d, a1, h - 1))
+
+
+def presums(d, a, h):
+    """Karatsuba operand leaves (3^h of them) for a level-h bitsliced operand."""
+    if h == 0:
+        return [a[0]]
+    half = 1 << (h - 1)
+    a0, a1 = a[:half], a[half:]
+    return presums(d, a0, h - 1) + presums(d, a1, h - 1) + presums(d, vadd(d, a0, a1), h - 1)
+
+
+def karatsuba(d, a, b, h):
+    """Recursive Karatsuba tower product (binary_tower.cuh:35-50), built depth-first so that
+    node creation order == a low-register-pressure evaluation order. `b` may be given as
+    prepared leaves (list of 3^h nodes, flag via tuple ('leaves', list))."""
+    if isinstance(b, tuple):
+        leaves = b[1]
+        if h == 0:
+            return [d.and_(a[0], leaves[0])]
+        n = 3 ** (h - 1)
+        half = 1 << (h - 1)
+        a0, a1 = a[:half], a[half:]
+        z0 = karatsuba(d, a0, ("leaves", leaves[:n]), h - 1)
+        z2 = karatsuba(d, a1, ("leaves", leaves[n:2 * n]), h - 1)
+        z1 = karatsuba(d, vadd(d, a0, a1), ("leaves", leaves[2 * n:]), h - 1)
+    else:
+        if h == 0:
+            return [d.and_(a[0], b[0])]
+        half = 1 << (h - 1)
+        a0, a1, b0, b1 = a[:half], a[half:], b[:half], b[half:]
+        z0 = karatsuba(d, a0, b0, h - 1)
+        z2 = karatsuba(d, a1, b1, h - 1)
+        z1 = karatsuba(d, vadd(d, a0, a1), vadd(d, b0, b1), h - 1)
+    lo = vadd(d, z0, z2)
+    hi = vadd(d, vadd(d, z1, lo), mul_alpha(d, z2, h - 1))
+    return lo + hi
+
+
+class Emitter:
+    """Emit a DAG as straight-line HIP with XOR3 / ANDXOR fusion."""
+
+    def __init__(self, dag, roots):
+        self.d = dag
+        self.roots = roots
+        uses = [0] * len(dag.nodes)
+        for i, (op, args) in enumerate(dag.nodes):
+            if op != "in":
+                for a in args:
+                    uses[a] += 1
+        for r in roots:
+            if r is not None:
+                uses[r] += 1
+        self.uses = uses
+
+    def emit(self, input_map, outputs):
+        """input_map: name -> C expression; outputs: list of (C lvalue, node or None)."""
+        d = self.d
+        live = set()
+        stack = [r for _, r in outputs if r is not None]
+        while stack:
+            n = stack.pop()
+            if n in live:
+                continue
+            live.add(n)
+            op, args = d.nodes[n]
+            if op != "in":
+                stack.extend(args)
+        # fusion decisions
+        absorbed = set()
+        fused = {}
+        for n in sorted(live):
+            op, args = d.nodes[n]
+            if op != "xor":
+                continue
+            a, b = args
+            cand = []
+            for x, y in ((a, b), (b, a)):
+                ox = d.nodes[x][0]
+                if self.uses[x] == 1 and x not in absorbed and x not in fused and ox in ("xor", "and"):
+                    cand.append((x, y))
+            # prefer absorbing an XOR (saves a full gate) over an AND
+            cand.sort(key=lambda t: 0 if d.nodes[t[0]][0] == "xor" else 1)
+            if cand:
+                x, y = cand[0]
+                absorbed.add(x)
+                fused[n] = (x, y)
+        lines = []
+        name = {}
+        cnt = [0]
+
+        def nm(n):
+            return name[n]
+
+        for n in sorted(live):
+            op, args = d.nodes[n]
+            if op == "in":
+                name[n] = input_map[args[0]]
+                continue
+            if n in absorbed:
+                continue
+            v = "t%d" % cnt[0]
+            cnt[0] += 1
+            if op == "and":
+                lines.append("const uint32_t %s = %s & %s;" % (v, nm(args[0]), nm(args[1])))
+            elif n in fused:
+                x, y = fused[n]
+                ox, xargs = d.nodes[x]
+                if ox == "xor":
+                    lines.append("const uint32_t %s = BN_XOR3(%s, %s, %s);" % (v, nm(xargs[0]), nm(xargs[1]), nm(y)))
+                else:
+                    lines.append("const uint32_t %s = BN_ANDXOR(%s, %s, %s);" % (v, nm(xargs[0]), nm(xargs[1]), nm(y)))
+            else:
+                lines.append("const uint32_t %s = %s ^ %s;" % (v, nm(args[0]), nm(args[1])))
+            name[n] = v
+        for lv, r in outputs:
+            lines.append("%s = %s;" % (lv, "0u" if r is None else nm(r)))
+        return lines
+
+
+def count_ops(lines):
+    return sum(1 for l in lines if l.startswith("const uint32_t t"))
+
+
+def gen_prep(h):
+    d = DAG()
+    w = [d.inp("w%d" % i) for i in range(1 << h)]
+    leaves = presums(d, w, h)
+    e = Emitter(d, leaves)
+    body = e.emit({"w%d" % i: "w[%d]" % i for i in range(1 << h)},
+                  [("wl[%d]" % i, leaves[i]) for i in range(len(leaves))])
+    return body
+
+
+def gen_mulp(h, accumulate=False):
+    """out = x * w  (or out ^= x*w when accumulate) given w's prepared leaves."""
+    d = DAG()
+    n = 1 << h
+    x = [d.inp("x%d" % i) for i in range(n)]
+    wl = [d.inp("wl%d" % i) for i in range(3 ** h)]
+    res = karatsuba(d, x, ("leaves", wl), h)
+    imap = {"x%d" % i: "x%d_" % i for i in range(n)}
+    imap.update({"wl%d" % i: "wl[%d]" % i for i in range(3 ** h)})
+    if accumulate:
+        acc = [d.inp("o%d" % i) for i in range(n)]
+        imap.update({"o%d" % i: "o%d_" % i for i in range(n)})
+        res = [d.xor(r, a) for r, a in zip(res, acc)]
+    e = Emitter(d, res)
+    body = e.emit(imap, [("out[%d]" % i, res[i]) for i in range(n)])
+    pre = ["const uint32_t x%d_ = x[%d];" % (i, i) for i in range(n)]
+    if accumulate:
+        pre += ["const uint32_t o%d_ = out[%d];" % (i, i) for i in range(n)]
+    return pre + body
+
+
+def gen_full(h):
+    """out = a * b, both bitsliced, alias-safe."""
+    d = DAG()
+    n = 1 << h
+    a = [d.inp("a%d" % i) for i in range(n)]
+    b = [d.inp("b%d" % i) for i in range(n)]
+    res = karatsuba(d, a, b, h)
+    imap = {"a%d" % i: "a%d_" % i for i in range(n)}
+    imap.update({"b%d" % i: "b%d_" % i for i in range(n)})
+    e = Emitter(d, res)
+    body = e.emit(imap, [("out[%d]" % i, res[i]) for i in range(n)])
+    pre = ["const uint32_t a%d_ = a[%d];" % (i, i) for i in range(n)]
+    pre += ["const uint32_t b%d_ = b[%d];" % (i, i) for i in range(n)]
+    return pre + body
+
+
+def fn(sig, lines):
+    return "__device__ __forceinline__ " + sig + " {\n\t" + "\n\t".join(lines) + "\n}\n"
+
+
+def main():
+    parts = ["// GENERATED by binius-ntt_amd/tools/gen_bitsliced.py -- do not edit.",
+             "// Bitsliced binary-tower multipliers (Karatsuba tower, gfx950 v_bitop3 fusion).",
+             "#pragma once", "#include <hip/hip_runtime.h>", "#include <stdint.h>", "",
+             "#define BN_XOR3(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x96)",
+             "#define BN_ANDXOR(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x6a)", "",
+             "namespace bn {", ""]
+    stats = []
+    for h in (2, 3, 4, 5):
+        pl = gen_prep(h)
+        parts.append("// prep: %d gates" % count_ops(pl))
+        parts.append(fn("void bsm%d_prep(const uint32_t* __restrict__ w, uint32_t* __restrict__ wl)" % h, pl))
+        ml = gen_mulp(h)
+        parts.append("// mulp: %d gates for 32 products" % count_ops(ml))
+        parts.append(fn("void bsm%d_mulp(const uint32_t* x, const uint32_t* __restrict__ wl, uint32_t* out)" % h, ml))
+        al = gen_mulp(h, accumulate=True)
+        parts.append("// mulp_acc (out ^= x*w): %d gates" % count_ops(al))
+        parts.append(fn("void bsm%d_mulp_acc(const uint32_t* x, const uint32_t* __restrict__ wl, uint32_t* out)" % h, al))
+        stats.append((h, count_ops(pl), count_ops(ml), count_ops(al)))
+    for h in (5, 7):
+        fl = gen_full(h)
+        parts.append("// full multiply: %d gates for 32 products" % count_ops(fl))
+        parts.append(fn("void bsm%d_mul(const uint32_t* a, const uint32_t* b, uint32_t* out)" % h, fl))
+        stats.append((h, "full", count_ops(fl)))
+    parts.append("}  // namespace bn")
+    with open(OUT, "w") as f:
+        f.write("\n".join(parts) + "\n")
+    for s in stats:
+        print(s, file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,143 @@
+/*
+ * binius_ntt_amd.h — the C-ABI drop-in boundary of the MI355X (gfx950) binary-tower /
+ * additive-NTT engine. Plain pointers and sizes only; every entry point returns an int
+ * status (0 = BN_OK) and never aborts; bn_last_error() describes the last failure on the
+ * calling thread.
+ *
+ * Each entry point names the reference interface it replaces (shourovrm/binius-NTT,
+ * paths relative to its repository root). The C++ mirror of the reference surface
+ * (AdditiveNTT<T,P>, NTTData, Sumcheck<N,d,T>, ...) lives in binius-ntt_amd/host/ulvt and
+ * calls only these functions.
+ *
+ * Element layouts (bit-exact with the reference):
+ *   GF(2^32) element  : one uint32_t.
+ *   GF(2^128) element : four uint32_t limbs, little-endian (limb 0 = bits 0..31),
+ *                       as src/ulvt/sumcheck/test/utils/bigints.cu:6-13.
+ *   bitsliced block   : 128 uint32_t words; word i holds bit i of 32 consecutive GF(2^128)
+ *                       elements, element e in bit e (src/ulvt/utils/bitslicing.cuh:32-47).
+ */
+#ifndef BINIUS_NTT_AMD_H
+#define BINIUS_NTT_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+	BN_OK = 0,
+	BN_ERR_INVALID = 1,     /* bad argument (reference: ASSERT / apply() returning false) */
+	BN_ERR_HIP = 2,         /* HIP runtime failure (reference: CUDA_CHECK, common.cuh:18-29) */
+	BN_ERR_UNSUPPORTED = 3, /* valid in the reference surface but not built here */
+	BN_ERR_ALLOC = 4        /* device or host allocation failure */
+};
+
+/* Description of the last error on this thread ("" if none). */
+const char* bn_last_error(void);
+/* Library version string. */
+const char* bn_version(void);
+
+/* Replaces bool check_gpu_capabilities() (src/ulvt/utils/common.cu:6-43): returns 1 if a
+ * gfx950 device with enough LDS for the kernels is visible, else 0. */
+int bn_check_gpu_capabilities(void);
+
+/* ------------------------------------------------------------------------------------
+ * Additive NTT (src/ulvt/ntt/additive_ntt.cuh, src/ulvt/ntt/nttconf.cuh)
+ * ------------------------------------------------------------------------------------ */
+typedef struct bn_antt_plan bn_antt_plan;
+
+/* Replaces AdditiveNTTConf<T,P>(log_h, log_rate) (nttconf.cuh:55-60) + the AdditiveNTT
+ * constructor (additive_ntt.cuh:178-199): validates 1 <= log_h, 0 <= log_rate <= 4,
+ * log_h + log_rate <= field_bits (and <= 32: every twiddle must lie in GF(2^32)),
+ * precomputes the normalised subspace evaluations on the host and stages them on
+ * `device`. field_bits is 32 (T=uint32_t, P=FanPaarTowerField<5>) or 128 (GF(2^128)). */
+int bn_antt_plan_create(int device, int field_bits, int log_h, int log_rate, bn_antt_plan** plan);
+/* Replaces ~AdditiveNTT (additive_ntt.cuh:267-270). NULL is accepted. */
+int bn_antt_plan_destroy(bn_antt_plan* plan);
+
+/* Replaces bool AdditiveNTT::apply(const NTTData<T>& in, NTTData<T>& out)
+ * (additive_ntt.cuh:201-265): host buffers, synchronous. in_elems must equal 2^log_h
+ * (the reference returns false otherwise: here BN_ERR_INVALID with no other effect);
+ * `out` receives 2^(log_h+log_rate) elements, coset-major. */
+int bn_antt_forward_host(bn_antt_plan* plan, const void* in, size_t in_elems, void* out);
+
+/* Device-resident entry (no reference counterpart; used by benchmarks, batched and
+ * multi-GPU callers): `batch` independent transforms, transform b reads
+ * d_in + b*2^log_h elements and writes d_out + b*2^(log_h+log_rate) elements.
+ * d_in and d_out must not overlap. Asynchronous on `stream` (a hipStream_t, may be 0). */
+int bn_antt_forward_device(bn_antt_plan* plan, const void* d_in, void* d_out, size_t batch, void* stream);
+
+/* Copies the plan's normalised subspace-evaluation table s[i][j] (GF(2^32) values,
+ * log_h rows x (log_h+log_rate-1) columns, row-major) to host memory. */
+int bn_antt_get_subspace_evals(const bn_antt_plan* plan, uint32_t* out, size_t out_words);
+
+/* Plan introspection: 0 log_h, 1 log_rate, 2 field_bits, 3 device, 4 kernel variant. */
+int bn_antt_plan_query(const bn_antt_plan* plan, int what, int64_t* value);
+
+/* Profiling hook for bench.py: records hipEvents around every kernel launch of the next
+ * bn_antt_forward_device call on its stream and returns per-launch-kind mean durations. */
+int bn_antt_set_event_timing(bn_antt_plan* plan, int enable);
+int bn_antt_get_event_timing(bn_antt_plan* plan, float* ms_per_kind, int max_kinds, int* n_kinds);
+
+/* ------------------------------------------------------------------------------------
+ * Binary tower field arithmetic (src/ulvt/finite_fields/)
+ * ------------------------------------------------------------------------------------ */
+/* Elementwise GF(2^128) product of compact vectors, n elements, device pointers.
+ * Semantics of tower_height_7_mul (src/ulvt/sumcheck/test/utils/tower_7_mul.cu:4-20). */
+int bn_gf128_mul_device(const void* d_a, const void* d_b, void* d_out, size_t n, void* stream);
+/* Same on bitsliced 128-word blocks: multiply_unrolled<7> (circuit_generator/unrolled/
+ * binary_tower_unrolled7.cu), n_blocks blocks of 32 products each. Alias-safe (d_out == d_a). */
+int bn_gf128_mul_bitsliced_device(const void* d_a, const void* d_b, void* d_out, size_t n_blocks, void* stream);
+/* Elementwise GF(2^32) product (FanPaarTowerField<5>::multiply, binary_tower.cuh:113-115). */
+int bn_gf32_mul_device(const void* d_a, const void* d_b, void* d_out, size_t n, void* stream);
+/* Register-resident repeat-loop microbenchmarks in the style of bitsliced_repeat
+ * (src/ulvt/finite_fields/tests/profiling/kernels/bitsliced_repeat.cu:5-32):
+ * kind 0 = compact GF(2^128), kind 1 = bitsliced GF(2^128) (32 products per lane-block).
+ * Each of `threads` lanes performs `iters` dependent products; d_state holds
+ * threads*4 (kind 0) or threads*128 (kind 1) words, updated in place. */
+int bn_gf128_mul_repeat_device(int kind, void* d_state, const void* d_operand, size_t threads, int iters, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Bitslicing (src/ulvt/utils/bitslicing.cuh:89-105)
+ * ------------------------------------------------------------------------------------ */
+/* In-place compact -> bitsliced (untranspose == 0) or bitsliced -> compact (untranspose != 0)
+ * over n_blocks 128-word blocks. Replaces transpose_kernel / untranspose_kernel. */
+int bn_bitslice_device(void* d_buf, size_t n_blocks, int untranspose, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Sumcheck over GF(2^128) (src/ulvt/sumcheck/sumcheck.cuh:10-301)
+ * ------------------------------------------------------------------------------------ */
+typedef struct bn_sumcheck bn_sumcheck;
+
+/* Replaces Sumcheck<NUM_VARS, COMPOSITION_SIZE, DATA_IS_TRANSPOSED>(evals, benchmarking)
+ * (sumcheck.cuh:82-126). evals: composition_size columns of 4*2^num_vars words each,
+ * column-major; compact when data_is_transposed == 0 (converted on the device), bitsliced
+ * 128-word blocks otherwise. 1 <= num_vars <= 30, 1 <= composition_size <= 8.
+ * The host copy is made synchronously. */
+int bn_sumcheck_create(int device, int num_vars, int composition_size, int data_is_transposed,
+                       const uint32_t* evals, bn_sumcheck** sc);
+/* As above but from device memory already holding the columns (no host copy). The buffer
+ * is copied into the prover's own storage unless take_ownership != 0, in which case the
+ * prover folds it in place and frees it with hipFree on destroy. */
+int bn_sumcheck_create_device(int device, int num_vars, int composition_size, int data_is_transposed,
+                              void* d_evals, int take_ownership, bn_sumcheck** sc);
+/* Replaces Sumcheck::this_round_messages(sum, points) (sumcheck.cuh:130-246):
+ * sum[4], points[4*(composition_size+1)] (round polynomial at 0..d). */
+int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32_t* points);
+/* Replaces Sumcheck::move_to_next_round(challenge) (sumcheck.cuh:248-300). */
+int bn_sumcheck_move_to_next_round(bn_sumcheck* sc, const uint32_t* challenge);
+/* Current round (0 .. num_vars). */
+int bn_sumcheck_round(const bn_sumcheck* sc, int* round);
+/* Multi-GPU sharding: this prover holds shard `rank` of `world` (interleaved by 32-element
+ * batch index); round messages are then partial and must be XOR-combined across ranks by
+ * the caller (the Python/RCCL layer does allgather + XOR). world must be a power of two
+ * with 32*world <= 2^num_vars. Must be called before the first round. */
+int bn_sumcheck_set_shard(bn_sumcheck* sc, int rank, int world);
+int bn_sumcheck_destroy(bn_sumcheck* sc);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,183 @@
+/*
+ * CPU ORACLE (test infrastructure only) — additive NTT.
+ * Restates src/ulvt/ntt/additive_ntt.cuh:
+ *   subspace_map            :16-19   x^2 + c*x
+ *   calculate_twiddle       :59-77   XOR of s[stage][k] over set bits of (coset<<(log_h-1-stage))|blk
+ *   antt_butterfly          :10-14   u += w*v ; v += u
+ *   additive_ntt_kernel     :91-160  stages end-1 .. start on a 2^stage butterfly block
+ *   AdditiveNTT::apply      :201-265 2^log_rate coset copies, kernels in reverse order,
+ *                                    coset-major output
+ *   precompute_subspace_evals :273-309
+ * The multi-launch / shared-memory tiling of the reference only changes the order in which
+ * independent butterflies run; the serial loop below computes the same values (pinned by
+ * the reference's MD5 table, test_ntt.cu:52-124).
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "oracle.h"
+
+#define SIDX(i, j, width) ((size_t)(i) * (size_t)(width) + (size_t)(j))
+
+void orc_subspace_evals32(int log_h, int log_rate, uint32_t* s) {
+	orc_init();
+	const int width = log_h + log_rate - 1;
+	uint32_t* norm = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(log_h > 0 ? log_h : 1));
+	memset(s, 0, sizeof(uint32_t) * (size_t)log_h * (size_t)(width > 0 ? width : 1));
+	for (int i = 1; i < log_h + log_rate; i++) s[SIDX(0, i - 1, width)] = 1u << i;
+	norm[0] = 1;
+	for (int i = 1; i < log_h; i++) {
+		uint32_t np = norm[i - 1];
+		uint32_t p0 = s[SIDX(i - 1, 0, width)];
+		norm[i] = (uint32_t)(orc_square(p0, 5) ^ orc_mul32(np, p0));
+		for (int j = 1; j < log_h + log_rate - i; j++) {
+			uint32_t sp = s[SIDX(i - 1, j, width)];
+			s[SIDX(i, j - 1, width)] = (uint32_t)(orc_square(sp, 5) ^ orc_mul32(np, sp));
+		}
+	}
+	for (int i = 0; i < log_h; i++) {
+		uint32_t inv = (uint32_t)orc_inv(norm[i], 5);
+		for (int j = 0; j < log_h + log_rate - i - 1; j++) s[SIDX(i, j, width)] = orc_mul32(inv, s[SIDX(i, j, width)]);
+	}
+	free(norm);
+}
+
+/* Same table computed with GF(2^128) arithmetic (the field policy P = GF(2^128)). */
+void orc_subspace_evals128(int log_h, int log_rate, uint32_t* s) {
+	orc_init();
+	const int width = log_h + log_rate - 1;
+	uint32_t(*norm)[4] = (uint32_t(*)[4])calloc((size_t)(log_h > 0 ? log_h : 1), sizeof(uint32_t[4]));
+	memset(s, 0, sizeof(uint32_t) * 4 * (size_t)log_h * (size_t)(width > 0 ? width : 1));
+	for (int i = 1; i < log_h + log_rate; i++) {
+		uint32_t* e = s + 4 * SIDX(0, i - 1, width);
+		e[i / 32] = 1u << (i % 32);   /* T(1 << i) as a 128-bit integer */
+	}
+	norm[0][0] = 1;
+	for (int i = 1; i < log_h; i++) {
+		uint32_t* np = norm[i - 1];
+		for (int j = 0; j < log_h + log_rate - i; j++) {
+			const uint32_t* sp = s + 4 * SIDX(i - 1, j, width);
+			uint32_t sq[4], t[4], r[4];
+			orc_mul128(sp, sp, sq);
+			orc_mul128(np, sp, t);
+			for (int k = 0; k < 4; k++) r[k] = sq[k] ^ t[k];
+			if (j == 0)
+				memcpy(norm[i], r, sizeof(r));
+			else
+				memcpy(s + 4 * SIDX(i, j - 1, width), r, sizeof(r));
+		}
+	}
+	for (int i = 0; i < log_h; i++) {
+		uint32_t inv[4];
+		orc_inv128(norm[i], inv);
+		for (int j = 0; j < log_h + log_rate - i - 1; j++) {
+			uint32_t* e = s + 4 * SIDX(i, j, width);
+			uint32_t r[4];
+			orc_mul128(inv, e, r);
+			memcpy(e, r, sizeof(r));
+		}
+	}
+	free(norm);
+}
+
+static inline uint32_t twiddle32(const uint32_t* s, int width, int log_h, int log_rate, int coset, int stage, size_t blk) {
+	uint64_t indicator = ((uint64_t)coset << (log_h - 1 - stage)) | (uint64_t)blk;
+	uint32_t sum = 0;
+	for (int k = 0; k < log_h + log_rate - 1 - stage; k++)
+		if ((indicator >> k) & 1) sum ^= s[SIDX(stage, k, width)];
+	return sum;
+}
+
+void orc_antt32(const uint32_t* in, uint32_t* out, int log_h, int log_rate) {
+	orc_init();
+	const int width = log_h + log_rate - 1;
+	uint32_t* s = (uint32_t*)calloc((size_t)log_h * (size_t)(width > 0 ? width : 1), sizeof(uint32_t));
+	orc_subspace_evals32(log_h, log_rate, s);
+	const size_t n = (size_t)1 << log_h;
+	for (int c = 0; c < (1 << log_rate); c++) {
+		uint32_t* d = out + (size_t)c * n;
+		memcpy(d, in, n * sizeof(uint32_t));
+		for (int stage = log_h - 1; stage >= 0; stage--) {
+			const size_t half = (size_t)1 << stage;
+			const size_t nblk = n >> (stage + 1);
+			for (size_t blk = 0; blk < nblk; blk++) {
+				uint32_t w = twiddle32(s, width, log_h, log_rate, c, stage, blk);
+				uint32_t* u = d + (blk << (stage + 1));
+				uint32_t* v = u + half;
+				for (size_t k = 0; k < half; k++) {
+					u[k] ^= orc_mul32(w, v[k]);
+					v[k] ^= u[k];
+				}
+			}
+		}
+	}
+	free(s);
+}
+
+void orc_antt128(const uint32_t* in, uint32_t* out, int log_h, int log_rate) {
+	orc_init();
+	const int width = log_h + log_rate - 1;
+	uint32_t* s = (uint32_t*)calloc(4 * (size_t)log_h * (size_t)(width > 0 ? width : 1), sizeof(uint32_t));
+	orc_subspace_evals128(log_h, log_rate, s);
+	const size_t n = (size_t)1 << log_h;
+	for (int c = 0; c < (1 << log_rate); c++) {
+		uint32_t* d = out + 4 * (size_t)c * n;
+		memcpy(d, in, 4 * n * sizeof(uint32_t));
+		for (int stage = log_h - 1; stage >= 0; stage--) {
+			const size_t half = (size_t)1 << stage;
+			const size_t nblk = n >> (stage + 1);
+			for (size_t blk = 0; blk < nblk; blk++) {
+				uint64_t indicator = ((uint64_t)c << (log_h - 1 - stage)) | (uint64_t)blk;
+				uint32_t w[4] = {0, 0, 0, 0};
+				for (int k = 0; k < log_h + log_rate - 1 - stage; k++)
+					if ((indicator >> k) & 1)
+						for (int q = 0; q < 4; q++) w[q] ^= s[4 * SIDX(stage, k, width) + q];
+				for (size_t k = 0; k < half; k++) {
+					uint32_t* u = d + 4 * ((blk << (stage + 1)) + k);
+					uint32_t* v = u + 4 * half;
+					uint32_t t[4];
+					orc_mul128(w, v, t);
+					for (int q = 0; q < 4; q++) {
+						u[q] ^= t[q];
+						v[q] ^= u[q];
+					}
+				}
+			}
+		}
+	}
+	free(s);
+}
+
+void orc_antt128_limbwise_batch(const uint32_t* in, uint32_t* out, int log_h, int log_rate, int batch) {
+	orc_init();
+	const int width = log_h + log_rate - 1;
+	uint32_t* s = (uint32_t*)calloc((size_t)log_h * (size_t)(width > 0 ? width : 1), sizeof(uint32_t));
+	orc_subspace_evals32(log_h, log_rate, s);
+	const size_t n = (size_t)1 << log_h;
+	for (int b = 0; b < batch; b++) {
+		const uint32_t* src = in + (size_t)b * 4 * n;
+		uint32_t* dstb = out + (size_t)b * 4 * n * ((size_t)1 << log_rate);
+		for (int c = 0; c < (1 << log_rate); c++) {
+			uint32_t* d = dstb + 4 * (size_t)c * n;
+			memcpy(d, src, 4 * n * sizeof(uint32_t));
+			for (int stage = log_h - 1; stage >= 0; stage--) {
+				const size_t half = (size_t)1 << stage;
+				const size_t nblk = n >> (stage + 1);
+				for (size_t blk = 0; blk < nblk; blk++) {
+					uint32_t w = twiddle32(s, width, log_h, log_rate, c, stage, blk);
+					uint32_t* u = d + 4 * (blk << (stage + 1));
+					uint32_t* v = u + 4 * half;
+					for (size_t k = 0; k < 4 * half; k++) {
+						u[k] ^= orc_mul32(w, v[k]);
+						v[k] ^= u[k];
+					}
+				}
+			}
+		}
+	}
+	free(s);
+}
+
+void orc_antt128_limbwise(const uint32_t* in, uint32_t* out, int log_h, int log_rate) {
+	orc_antt128_limbwise_batch(in, out, log_h, log_rate, 1);
+}

@@ -1,0 +1,98 @@
+"""GPU parity for the additive NTT: HIP path (through the C-ABI) vs the oracle and the
+reference's own golden MD5 table (src/ulvt/ntt/tests/test_ntt.cu:52-124, 191-234)."""
+import numpy as np
+import pytest
+
+import _oracle as O
+import binius_ntt_amd as B
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_device(ntt, x_np, dev, batch=1):
+    import torch
+    x = torch.from_numpy(x_np.astype(np.uint32).view(np.int32)).to(dev)
+    n_out = x_np.size << ntt.conf.log_rate
+    y = torch.empty(n_out, dtype=torch.int32, device=dev)
+    ntt.forward_device(x, y, batch=batch)
+    torch.cuda.synchronize()
+    return y.cpu().numpy().view(np.uint32)
+
+
+def test_capabilities():
+    assert B.check_gpu_capabilities(), B.lib().bn_last_error()
+
+
+@pytest.mark.parametrize("log_h", list(range(1, 25)))
+def test_gf32_r0_reference_md5(ntt_md5, log_h, dev):
+    # exactly the reference's run_and_check_additive_ntt(log_h, 0) (test_ntt.cu:191-217)
+    x = O.mt_fill(0xDEADBEEF + log_h, 1 << log_h)
+    ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(5)))
+    inp = B.NTTData(1 << log_h, B.DataOrder.IN_ORDER, 32, x)
+    out = B.NTTData(1 << log_h, field_bits=32)
+    assert ntt.apply(inp, out)
+    assert out.order == B.DataOrder.IN_ORDER
+    assert O.md5(out.data) == ntt_md5["0"][log_h]
+
+
+@pytest.mark.parametrize("log_h", list(range(1, 23)))
+def test_gf32_r2_reference_md5(ntt_md5, log_h, dev):
+    x = O.mt_fill(0xDEADBEEF + log_h + 2, 1 << log_h)
+    ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 2, B.FanPaarTowerField(5)))
+    y = _run_device(ntt, x, dev)
+    assert O.md5(y) == ntt_md5["2"][log_h]
+
+
+@pytest.mark.parametrize("log_h,r", [(1, 0), (2, 1), (3, 0), (5, 2), (8, 0), (10, 0), (10, 2), (11, 1),
+                                     (12, 3), (13, 0), (14, 4), (16, 0), (17, 2), (20, 0)])
+def test_gf128_matches_oracle(log_h, r, dev):
+    # independent random limbs (equal limbs would hide limb-swap bugs)
+    x = O.fill128(0xDEADBEEF + log_h + r, 0x5EED0000, 1 << log_h)
+    ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, r, B.FanPaarTowerField(7)))
+    y = _run_device(ntt, x.reshape(-1), dev).reshape(-1, 4)
+    assert np.array_equal(y, O.antt128(x, log_h, r))
+
+
+def test_gf128_apply_host_semantics(dev):
+    ntt = B.AdditiveNTT(B.AdditiveNTTConf(10, 1, B.FanPaarTowerField(7)))
+    x = O.fill128(1, 2, 1 << 10)
+    bad = B.NTTData(1 << 9, B.DataOrder.IN_ORDER, 128)
+    out = B.NTTData(1 << 11, field_bits=128)
+    assert not ntt.apply(bad, out)  # wrong size -> False, no other effect
+    wrong_order = B.NTTData(1 << 10, B.DataOrder.BIT_REVERSED, 128, x)
+    assert not ntt.apply(wrong_order, out)
+    good = B.NTTData(1 << 10, B.DataOrder.IN_ORDER, 128, x)
+    assert ntt.apply(good, out)
+    assert np.array_equal(out.data, O.antt128(x, 10, 1))
+
+
+def test_gf128_batched(dev):
+    log_h, batch = 12, 5
+    xs = np.stack([O.fill128(100 + b, 200 + b, 1 << log_h) for b in range(batch)])
+    ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(7)))
+    y = _run_device(ntt, xs.reshape(-1), dev, batch=batch).reshape(batch, -1, 4)
+    assert np.array_equal(y, O.antt128_batch(xs, log_h, 0))
+
+
+@pytest.mark.slow
+def test_gf128_north_star_size_limb_md5_and_oracle(ntt_md5, dev):
+    # 2^24: limb 0 = the reference's mt19937 stream (MD5-pinned by the reference table),
+    # limbs 1..3 = independent mt19937_64 streams (checked against the oracle).
+    log_h = 24
+    x = O.fill128(0xDEADBEEF + log_h, 0x5EED0000, 1 << log_h)
+    ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(7)))
+    y = _run_device(ntt, x.reshape(-1), dev).reshape(-1, 4)
+    assert O.md5_limb(y, 0) == ntt_md5["0"][log_h]
+    assert np.array_equal(y, O.antt128(x, log_h, 0))
+
+
+def test_gf128_linearity_at_2_20(dev):
+    # size-independent property: NTT(a ^ b) == NTT(a) ^ NTT(b)
+    log_h = 20
+    a = O.fill128(5, 6, 1 << log_h)
+    b = O.fill128(7, 8, 1 << log_h)
+    ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(7)))
+    ya = _run_device(ntt, a.reshape(-1), dev)
+    yb = _run_device(ntt, b.reshape(-1), dev)
+    yab = _run_device(ntt, (a ^ b).reshape(-1), dev)
+    assert np.array_equal(ya ^ yb, yab)
