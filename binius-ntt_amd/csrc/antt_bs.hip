@@ -1,12 +1,346 @@
-// Bitsliced fast path for the additive NTT (placeholder: not yet enabled).
+// Bitsliced, LDS-tiled additive NTT for gfx950 (kernel variant 1).
+//
+// Data layout
+//   * A "block" is 32 consecutive elements. In bitsliced form (the same layout as the
+//     reference's BitsliceUtils<128>, src/ulvt/utils/bitslicing.cuh:32-47) block word
+//     32*l + i holds bit i of limb l of the 32 elements, element e in bit e.
+//   * Between passes the transform lives in HBM as bitsliced blocks in element order (our own
+//     scratch layout); the first pass reads the caller's compact AoS input and the last pass
+//     writes compact AoS output, so exactly two bit-transposes happen per transform.
+//   * A workgroup owns a tile of 256 blocks (2^13 elements, 144 KiB of LDS at GF(2^128)):
+//     index bits 0..4 (inside each word) plus 8 "block bits" bb[0..7]; the remaining index
+//     bits are fixed per workgroup.
+//
+// Arithmetic
+//   Every twiddle lies in GF(2^32) and multiplies each GF(2^32) limb separately, so a
+//   GF(2^128) butterfly is four GF(2^32) bitsliced butterflies sharing one twiddle. Products
+//   use the generated Karatsuba circuits (bitsliced_gen.hpp, v_bitop3-fused); when every
+//   twiddle a wave needs lies in GF(2^8) or GF(2^16) the cheaper sub-field circuits are used
+//   (multiplication by a sub-field scalar acts on each sub-field coordinate independently).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
 #include "antt_plan.hpp"
+#include "bitsliced.hpp"
 
 namespace bn {
 
-bool bs_supports(const bn_antt_plan*) { return false; }
-int bs_prepare(bn_antt_plan*) { return BN_OK; }
-int launch_bs(bn_antt_plan*, const uint32_t*, uint32_t*, size_t, hipStream_t) {
-	BN_FAIL(BN_ERR_UNSUPPORTED, "bitsliced path not built");
+constexpr int kBlkBits = 8;
+constexpr int kTileBlocks = 1 << kBlkBits;
+constexpr int kLimbStride = 36;  // LDS words per (block, limb): 32 + 4 pad (bank spread)
+constexpr int kMinLogH = 13;
+
+struct BsPass {
+	int lo, k;
+	int in_compact, out_compact, first;
+	int bb[kBlkBits];       // index bit of tile block bit m
+	int stage_m[kBlkBits];  // block bit m of stage (lo + j), j < k, for stages >= 5
+	int ob[32];             // outer index bits, ascending
+	int n_outer;
+};
+
+struct BsParams {
+	const uint32_t* src;
+	uint32_t* dst;
+	const uint32_t* s;
+	int width, log_h, log_rate;
+	BsPass p;
+};
+
+// bit masks of the bit-lanes p with bit j of p set
+__device__ __forceinline__ uint32_t lane_mask(int j) {
+	return j == 0 ? 0xAAAAAAAAu : j == 1 ? 0xCCCCCCCCu : j == 2 ? 0xF0F0F0F0u : j == 3 ? 0xFF00FF00u : 0xFFFF0000u;
+}
+
+// u ^= w*v for 32 bitsliced GF(2^32) limbs, twiddle words W (bit i of the twiddle per lane),
+// choosing the smallest sub-field circuit that holds every twiddle of this wave.
+__device__ __forceinline__ void mul_acc_tw(const uint32_t* v, const uint32_t* W, uint32_t* u) {
+	uint32_t hi16 = 0, hi8 = 0;
+#pragma unroll
+	for (int i = 16; i < 32; i++) hi16 |= W[i];
+#pragma unroll
+	for (int i = 8; i < 16; i++) hi8 |= W[i];
+	if (!__any(hi16 != 0)) {
+		if (!__any(hi8 != 0)) {
+#pragma unroll
+			for (int g = 0; g < 4; g++) bsm3_mul_acc(v + 8 * g, W, u + 8 * g);
+		} else {
+#pragma unroll
+			for (int g = 0; g < 2; g++) bsm4_mul_acc(v + 16 * g, W, u + 16 * g);
+		}
+	} else {
+		bsm5_mul_acc(v, W, u);
+	}
+}
+
+// out = w*x (alias-safe: out may be x), same sub-field dispatch as mul_acc_tw.
+__device__ __forceinline__ void mul_tw(const uint32_t* x, const uint32_t* W, uint32_t* out) {
+	uint32_t hi16 = 0, hi8 = 0;
+#pragma unroll
+	for (int i = 16; i < 32; i++) hi16 |= W[i];
+#pragma unroll
+	for (int i = 8; i < 16; i++) hi8 |= W[i];
+	if (!__any(hi16 != 0)) {
+		if (!__any(hi8 != 0)) {
+#pragma unroll
+			for (int g = 0; g < 4; g++) bsm3_mul(x + 8 * g, W, out + 8 * g);
+		} else {
+#pragma unroll
+			for (int g = 0; g < 2; g++) bsm4_mul(x + 16 * g, W, out + 16 * g);
+		}
+	} else {
+		bsm5_mul(x, W, out);
+	}
+}
+
+template <int L>
+__global__ __launch_bounds__(128 * L) void antt_bs_pass(BsParams P) {
+	extern __shared__ uint32_t lds[];
+	constexpr int BLK_WORDS = L * kLimbStride;
+	constexpr int NT = 128 * L;
+	const BsPass& ps = P.p;
+	const int tid = threadIdx.x;
+	const size_t n = (size_t)1 << P.log_h;
+
+	// ---- workgroup -> (batch, coset, outer bits)
+	const size_t bid = blockIdx.x;
+	const size_t outer = bid & (((size_t)1 << ps.n_outer) - 1);
+	const size_t rest = bid >> ps.n_outer;
+	const int coset = (int)(rest & ((1u << P.log_rate) - 1));
+	const size_t batch = rest >> P.log_rate;
+	size_t outer_off = 0;
+	for (int m = 0; m < ps.n_outer; m++) outer_off |= ((outer >> m) & 1) << ps.ob[m];
+	auto block_idx = [&](int q) -> size_t {
+		size_t off = outer_off;
+#pragma unroll
+		for (int m = 0; m < kBlkBits; m++) off |= (size_t)((q >> m) & 1) << ps.bb[m];
+		return off;
+	};
+	uint32_t* dst = P.dst + (((batch << P.log_rate) + (size_t)coset) * n) * L;
+	const uint32_t* src = ps.first ? (P.src + batch * n * L) : dst;
+
+	// ---- load tile into LDS (coalesced 16-byte loads; compact input is split by limb)
+	for (int u = tid; u < kTileBlocks * 8 * L; u += NT) {
+		const int q = u / (8 * L), j = u % (8 * L);
+		const uint4 g = *(const uint4*)(src + block_idx(q) * L + 4 * j);
+		uint32_t* b = lds + q * BLK_WORDS;
+		if (ps.in_compact) {
+			const uint32_t w[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+			for (int t = 0; t < 4; t++) {
+				const int word = 4 * j + t;
+				b[(word % L) * kLimbStride + word / L] = w[t];
+			}
+		} else {
+			const int l = (4 * j) / 32, i = (4 * j) % 32;
+			*(uint4*)(b + l * kLimbStride + i) = g;
+		}
+	}
+	__syncthreads();
+	if (ps.in_compact) {
+		for (int u = tid; u < kTileBlocks * L; u += NT) {
+			uint32_t* x = lds + (u / L) * BLK_WORDS + (u % L) * kLimbStride;
+			uint32_t r[32];
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) *(uint4*)(r + i) = *(const uint4*)(x + i);
+			transpose32(r);
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) *(uint4*)(x + i) = *(const uint4*)(r + i);
+		}
+		__syncthreads();
+	}
+
+	// ---- stages, high to low
+	for (int j = ps.k - 1; j >= 0; j--) {
+		const int s = ps.lo + j;
+		const uint32_t* srow = P.s + (size_t)s * P.width;
+		const int nbits = P.log_h + P.log_rate - 1 - s;
+		if (s >= 5) {
+			// block-bit stage: one thread per (block pair, limb)
+			const int m = ps.stage_m[j];
+			const int pair = tid / L, l = tid % L;
+			const int qu = ((pair >> m) << (m + 1)) | (pair & ((1 << m) - 1));
+			const int qv = qu | (1 << m);
+			const uint64_t ind = ((uint64_t)coset << (P.log_h - 1 - s)) | (uint64_t)(block_idx(qu) >> (s + 1));
+			uint32_t w = 0;
+			for (int kk = 0; kk < nbits; kk++) w ^= ((ind >> kk) & 1) ? srow[kk] : 0u;
+			uint32_t W[32], U[32], V[32];
+#pragma unroll
+			for (int i = 0; i < 32; i++) W[i] = 0u - ((w >> i) & 1u);
+			uint32_t* pu = lds + qu * BLK_WORDS + l * kLimbStride;
+			uint32_t* pv = lds + qv * BLK_WORDS + l * kLimbStride;
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) {
+				*(uint4*)(U + i) = *(const uint4*)(pu + i);
+				*(uint4*)(V + i) = *(const uint4*)(pv + i);
+			}
+			mul_acc_tw(V, W, U);
+#pragma unroll
+			for (int i = 0; i < 32; i++) V[i] ^= U[i];
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) {
+				*(uint4*)(pu + i) = *(const uint4*)(U + i);
+				*(uint4*)(pv + i) = *(const uint4*)(V + i);
+			}
+		} else {
+			// intra-word stage: pairs are bit-lanes p, p + 2^s of the same word
+			const int d = 1 << s;
+			const uint32_t um = ~lane_mask(s);
+			// twiddle of bit-lane p: sum_k blk_k srow[k], blk = (block_base + p) >> (s+1);
+			// blk bits below 4-s come from p (bit-lane patterns), the rest from the block.
+			uint32_t pat[32];
+#pragma unroll
+			for (int i = 0; i < 32; i++) pat[i] = 0;
+			for (int kk = 0; kk < 4 - s; kk++) {
+				const uint32_t t = srow[kk], mk = lane_mask(s + 1 + kk);
+#pragma unroll
+				for (int i = 0; i < 32; i++) pat[i] ^= ((t >> i) & 1u) ? mk : 0u;
+			}
+			for (int u = tid; u < kTileBlocks * L; u += NT) {
+				const int q = u / L, l = u % L;
+				const uint64_t ind = ((uint64_t)coset << (P.log_h - 1 - s)) | (uint64_t)(block_idx(q) >> (s + 1));
+				uint32_t c = 0;
+				for (int kk = 4 - s; kk < nbits; kk++) c ^= ((ind >> kk) & 1) ? srow[kk] : 0u;
+				uint32_t W[32], X[32], T[32];
+#pragma unroll
+				for (int i = 0; i < 32; i++) W[i] = pat[i] ^ (0u - ((c >> i) & 1u));
+				uint32_t* px = lds + q * BLK_WORDS + l * kLimbStride;
+#pragma unroll
+				for (int i = 0; i < 32; i += 4) *(uint4*)(X + i) = *(const uint4*)(px + i);
+#pragma unroll
+				for (int i = 0; i < 32; i++) T[i] = X[i] >> d;
+				mul_tw(T, W, T);
+#pragma unroll
+				for (int i = 0; i < 32; i++) {
+					X[i] ^= T[i] & um;
+					X[i] ^= (X[i] & um) << d;
+				}
+#pragma unroll
+				for (int i = 0; i < 32; i += 4) *(uint4*)(px + i) = *(const uint4*)(X + i);
+			}
+		}
+		__syncthreads();
+	}
+
+	// ---- store tile
+	if (ps.out_compact) {
+		for (int u = tid; u < kTileBlocks * L; u += NT) {
+			uint32_t* x = lds + (u / L) * BLK_WORDS + (u % L) * kLimbStride;
+			uint32_t r[32];
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) *(uint4*)(r + i) = *(const uint4*)(x + i);
+			transpose32(r);
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) *(uint4*)(x + i) = *(const uint4*)(r + i);
+		}
+		__syncthreads();
+	}
+	for (int u = tid; u < kTileBlocks * 8 * L; u += NT) {
+		const int q = u / (8 * L), j = u % (8 * L);
+		const uint32_t* b = lds + q * BLK_WORDS;
+		uint4 g;
+		if (ps.out_compact) {
+			uint32_t w[4];
+#pragma unroll
+			for (int t = 0; t < 4; t++) {
+				const int word = 4 * j + t;
+				w[t] = b[(word % L) * kLimbStride + word / L];
+			}
+			g = make_uint4(w[0], w[1], w[2], w[3]);
+		} else {
+			const int l = (4 * j) / 32, i = (4 * j) % 32;
+			g = *(const uint4*)(b + l * kLimbStride + i);
+		}
+		*(uint4*)(dst + block_idx(q) * L + 4 * j) = g;
+	}
+}
+
+// ------------------------------------------------------------------------------------
+// host: pass planning
+// ------------------------------------------------------------------------------------
+static std::vector<BsPass> plan_passes(int log_h) {
+	std::vector<BsPass> passes;
+	// bottom pass: contiguous 2^13-element tiles, stages 0..12
+	auto make = [&](int lo, int k, bool bottom) {
+		BsPass p{};
+		p.lo = lo;
+		p.k = k;
+		std::vector<int> bits;
+		if (bottom) {
+			for (int b = 5; b < 5 + kBlkBits; b++) bits.push_back(b);
+		} else {
+			// stage bits plus the lowest non-word batch bits (adjacent blocks in memory)
+			for (int b = 5; (int)bits.size() < kBlkBits - k; b++) bits.push_back(b);
+			for (int b = lo; b < lo + k; b++) bits.push_back(b);
+		}
+		for (int m = 0; m < kBlkBits; m++) p.bb[m] = bits[m];
+		for (int j = 0; j < k; j++) {
+			p.stage_m[j] = -1;
+			for (int m = 0; m < kBlkBits; m++)
+				if (p.bb[m] == lo + j) p.stage_m[j] = m;
+		}
+		p.n_outer = 0;
+		for (int b = 5; b < log_h; b++)
+			if (std::find(bits.begin(), bits.end(), b) == bits.end()) p.ob[p.n_outer++] = b;
+		return p;
+	};
+	const int rest = log_h - kMinLogH;
+	const int n_up = (rest + kBlkBits - 1) / kBlkBits;
+	// upper passes, executed first (highest stages first)
+	int hi = log_h;
+	for (int i = 0; i < n_up; i++) {
+		const int remaining_up = n_up - i;
+		const int k = (hi - kMinLogH + remaining_up - 1) / remaining_up;
+		passes.push_back(make(hi - k, k, false));
+		hi -= k;
+	}
+	passes.push_back(make(0, kMinLogH, true));
+	for (size_t i = 0; i < passes.size(); i++) {
+		passes[i].first = i == 0;
+		passes[i].in_compact = i == 0;
+		passes[i].out_compact = i + 1 == passes.size();
+	}
+	return passes;
+}
+
+bool bs_supports(const bn_antt_plan* plan) { return plan->log_h >= kMinLogH; }
+
+int bs_prepare(bn_antt_plan* plan) {
+	const size_t lds4 = (size_t)kTileBlocks * 4 * kLimbStride * sizeof(uint32_t);
+	const size_t lds1 = (size_t)kTileBlocks * 1 * kLimbStride * sizeof(uint32_t);
+	BN_HIP(hipFuncSetAttribute((const void*)antt_bs_pass<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds4));
+	BN_HIP(hipFuncSetAttribute((const void*)antt_bs_pass<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
+	plan->variant = 1;
+	return BN_OK;
+}
+
+int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st) {
+	const auto passes = plan_passes(plan->log_h);
+	const int L = plan->limbs;
+	for (size_t i = 0; i < passes.size(); i++) {
+		BsParams prm;
+		prm.src = d_in;
+		prm.dst = d_out;
+		prm.s = plan->s_dev;
+		prm.width = plan->width;
+		prm.log_h = plan->log_h;
+		prm.log_rate = plan->log_rate;
+		prm.p = passes[i];
+		const size_t grid = (batch << plan->log_rate) << passes[i].n_outer;
+		const size_t lds = (size_t)kTileBlocks * L * kLimbStride * sizeof(uint32_t);
+		int rc = timing_begin(plan, (int)i, st);
+		if (rc != BN_OK) return rc;
+		if (L == 4)
+			hipLaunchKernelGGL(antt_bs_pass<4>, dim3((unsigned)grid), dim3(512), lds, st, prm);
+		else
+			hipLaunchKernelGGL(antt_bs_pass<1>, dim3((unsigned)grid), dim3(128), lds, st, prm);
+		BN_HIP(hipGetLastError());
+		rc = timing_end(plan, (int)i, st);
+		if (rc != BN_OK) return rc;
+	}
+	return BN_OK;
 }
 
 }  // namespace bn

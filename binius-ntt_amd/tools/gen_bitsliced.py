@@ -222,8 +222,8 @@ def gen_mulp(h, accumulate=False):
     return pre + body
 
 
-def gen_full(h):
-    """out = a * b, both bitsliced, alias-safe."""
+def gen_full(h, accumulate=False):
+    """out = a * b (or out ^= a * b), both bitsliced, alias-safe."""
     d = DAG()
     n = 1 << h
     a = [d.inp("a%d" % i) for i in range(n)]
@@ -231,10 +231,16 @@ def gen_full(h):
     res = karatsuba(d, a, b, h)
     imap = {"a%d" % i: "a%d_" % i for i in range(n)}
     imap.update({"b%d" % i: "b%d_" % i for i in range(n)})
+    if accumulate:
+        acc = [d.inp("o%d" % i) for i in range(n)]
+        imap.update({"o%d" % i: "o%d_" % i for i in range(n)})
+        res = [d.xor(r, q) for r, q in zip(res, acc)]
     e = Emitter(d, res)
     body = e.emit(imap, [("out[%d]" % i, res[i]) for i in range(n)])
     pre = ["const uint32_t a%d_ = a[%d];" % (i, i) for i in range(n)]
     pre += ["const uint32_t b%d_ = b[%d];" % (i, i) for i in range(n)]
+    if accumulate:
+        pre += ["const uint32_t o%d_ = out[%d];" % (i, i) for i in range(n)]
     return pre + body
 
 
@@ -261,11 +267,16 @@ def main():
         parts.append("// mulp_acc (out ^= x*w): %d gates" % count_ops(al))
         parts.append(fn("void bsm%d_mulp_acc(const uint32_t* x, const uint32_t* __restrict__ wl, uint32_t* out)" % h, al))
         stats.append((h, count_ops(pl), count_ops(ml), count_ops(al)))
-    for h in (5, 7):
+    for h in (3, 4, 5, 7):
         fl = gen_full(h)
         parts.append("// full multiply: %d gates for 32 products" % count_ops(fl))
         parts.append(fn("void bsm%d_mul(const uint32_t* a, const uint32_t* b, uint32_t* out)" % h, fl))
         stats.append((h, "full", count_ops(fl)))
+        if h < 7:
+            fa = gen_full(h, accumulate=True)
+            parts.append("// full multiply-accumulate (out ^= a*b): %d gates" % count_ops(fa))
+            parts.append(fn("void bsm%d_mul_acc(const uint32_t* a, const uint32_t* b, uint32_t* out)" % h, fa))
+            stats.append((h, "full_acc", count_ops(fa)))
     parts.append("}  // namespace bn")
     with open(OUT, "w") as f:
         f.write("\n".join(parts) + "\n")
