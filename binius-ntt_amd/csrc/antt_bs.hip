@@ -36,9 +36,10 @@ struct BsPass {
 	int lo, k;
 	int in_compact, out_compact, first;
 	int bb[kBlkBits];       // index bit of tile block bit m
-	int stage_m[kBlkBits];  // block bit m of stage (lo + j), j < k, for stages >= 5
+	int stage_m[32];        // block bit m of stage (lo + j), j < k, for stages >= 5
 	int ob[32];             // outer index bits, ascending
 	int n_outer;
+	int stop_j;  // debug: lowest local stage processed (normally 0)
 };
 
 struct BsParams {
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(128 * L) void antt_bs_pass(BsParams P) {
 	}
 
 	// ---- stages, high to low
-	for (int j = ps.k - 1; j >= 0; j--) {
+	for (int j = ps.k - 1; j >= ps.stop_j; j--) {
 		const int s = ps.lo + j;
 		const uint32_t* srow = P.s + (size_t)s * P.width;
 		const int nbits = P.log_h + P.log_rate - 1 - s;
@@ -319,7 +320,10 @@ int bs_prepare(bn_antt_plan* plan) {
 int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st) {
 	const auto passes = plan_passes(plan->log_h);
 	const int L = plan->limbs;
-	for (size_t i = 0; i < passes.size(); i++) {
+	// debug hook: BN_DEBUG_MAX_PASSES=n runs only the first n passes
+	size_t npass = passes.size();
+	if (const char* e = getenv("BN_DEBUG_MAX_PASSES")) npass = std::min(npass, (size_t)atoi(e));
+	for (size_t i = 0; i < npass; i++) {
 		BsParams prm;
 		prm.src = d_in;
 		prm.dst = d_out;
@@ -328,6 +332,9 @@ int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t 
 		prm.log_h = plan->log_h;
 		prm.log_rate = plan->log_rate;
 		prm.p = passes[i];
+		prm.p.stop_j = 0;
+		if (const char* e = getenv("BN_DEBUG_STOP_STAGE"))  // debug: run stages >= this only
+			prm.p.stop_j = std::max(0, std::min(prm.p.k, atoi(e) - prm.p.lo));
 		const size_t grid = (batch << plan->log_rate) << passes[i].n_outer;
 		const size_t lds = (size_t)kTileBlocks * L * kLimbStride * sizeof(uint32_t);
 		int rc = timing_begin(plan, (int)i, st);
