@@ -7,9 +7,9 @@
 //   * Between passes the transform lives in HBM as bitsliced blocks in element order (our own
 //     scratch layout); the first pass reads the caller's compact AoS input and the last pass
 //     writes compact AoS output, so exactly two bit-transposes happen per transform.
-//   * A workgroup owns a tile of 256 blocks (2^13 elements, 144 KiB of LDS at GF(2^128)):
-//     index bits 0..4 (inside each word) plus 8 "block bits" bb[0..7]; the remaining index
-//     bits are fixed per workgroup.
+//   * A workgroup owns a tile of 128 blocks (2^12 elements, 72 KiB of LDS at GF(2^128), two
+//     workgroups per CU so one loads/stores while the other computes): index bits 0..4 inside
+//     each word plus 7 "block bits" bb[0..6]; the remaining index bits are fixed per workgroup.
 //
 // Arithmetic
 //   Every twiddle lies in GF(2^32) and multiplies each GF(2^32) limb separately, so a
@@ -17,6 +17,9 @@
 //   use the generated Karatsuba circuits (bitsliced_gen.hpp, v_bitop3-fused); when every
 //   twiddle a wave needs lies in GF(2^8) or GF(2^16) the cheaper sub-field circuits are used
 //   (multiplication by a sub-field scalar acts on each sub-field coordinate independently).
+//   Twiddles are linear in the block index (calculate_twiddle, additive_ntt.cuh:59-77), so
+//   the workgroup-uniform part (coset + fixed index bits) and the per-thread part (tile bits)
+//   are summed separately.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -27,19 +30,21 @@
 
 namespace bn {
 
-constexpr int kBlkBits = 8;
+constexpr int kBlkBits = 7;
 constexpr int kTileBlocks = 1 << kBlkBits;
 constexpr int kLimbStride = 36;  // LDS words per (block, limb): 32 + 4 pad (bank spread)
-constexpr int kMinLogH = 13;
+constexpr int kMinLogH = kBlkBits + 5;
+
+enum { ROLE_FIRST = 0, ROLE_MID = 1, ROLE_LAST = 2, ROLE_SINGLE = 3 };
 
 struct BsPass {
 	int lo, k;
-	int in_compact, out_compact, first;
-	int bb[kBlkBits];       // index bit of tile block bit m
-	int stage_m[32];        // block bit m of stage (lo + j), j < k, for stages >= 5
-	int ob[32];             // outer index bits, ascending
+	int bb[kBlkBits];  // index bit of tile block bit m
+	int stage_m[32];   // block bit m of stage (lo + j), j < k, for stages >= 5
+	int ob[32];        // outer index bits, ascending
 	int n_outer;
-	int stop_j;  // debug: lowest local stage processed (normally 0)
+	int stop_j;        // debug: lowest local stage processed (normally 0)
+	int role;
 };
 
 struct BsParams {
@@ -49,6 +54,21 @@ struct BsParams {
 	int width, log_h, log_rate;
 	BsPass p;
 };
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// streaming (non-temporal) 16-byte global accesses: every byte is touched once per pass
+__device__ __forceinline__ uint4 ld_stream(const uint32_t* p) {
+	const u32x4 v = __builtin_nontemporal_load((const u32x4*)p);
+	return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_stream(uint32_t* p, uint4 g) {
+	u32x4 v;
+	v.x = g.x;
+	v.y = g.y;
+	v.z = g.z;
+	v.w = g.w;
+	__builtin_nontemporal_store(v, (u32x4*)p);
+}
 
 // bit masks of the bit-lanes p with bit j of p set
 __device__ __forceinline__ uint32_t lane_mask(int j) {
@@ -96,11 +116,13 @@ __device__ __forceinline__ void mul_tw(const uint32_t* x, const uint32_t* W, uin
 	}
 }
 
-template <int L>
-__global__ __launch_bounds__(128 * L) void antt_bs_pass(BsParams P) {
+template <int L, int ROLE>
+__global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 	extern __shared__ uint32_t lds[];
 	constexpr int BLK_WORDS = L * kLimbStride;
-	constexpr int NT = 128 * L;
+	constexpr int NT = 64 * L;
+	constexpr bool IN_COMPACT = ROLE == ROLE_FIRST || ROLE == ROLE_SINGLE;
+	constexpr bool OUT_COMPACT = ROLE == ROLE_LAST || ROLE == ROLE_SINGLE;
 	const BsPass& ps = P.p;
 	const int tid = threadIdx.x;
 	const size_t n = (size_t)1 << P.log_h;
@@ -113,21 +135,32 @@ __global__ __launch_bounds__(128 * L) void antt_bs_pass(BsParams P) {
 	const size_t batch = rest >> P.log_rate;
 	size_t outer_off = 0;
 	for (int m = 0; m < ps.n_outer; m++) outer_off |= ((outer >> m) & 1) << ps.ob[m];
-	auto block_idx = [&](int q) -> size_t {
-		size_t off = outer_off;
+	auto tile_off = [&](int q) -> size_t {
+		size_t off = 0;
 #pragma unroll
 		for (int m = 0; m < kBlkBits; m++) off |= (size_t)((q >> m) & 1) << ps.bb[m];
 		return off;
 	};
 	uint32_t* dst = P.dst + (((batch << P.log_rate) + (size_t)coset) * n) * L;
-	const uint32_t* src = ps.first ? (P.src + batch * n * L) : dst;
+	const uint32_t* src = IN_COMPACT ? (P.src + batch * n * L) : dst;
 
-	// ---- load tile into LDS (coalesced 16-byte loads; compact input is split by limb)
-	for (int u = tid; u < kTileBlocks * 8 * L; u += NT) {
+	// ---- load tile into LDS (coalesced 16-byte loads, all issued before the first LDS write;
+	//      compact input is split by limb)
+	constexpr int LOADS = kTileBlocks * 8 * L / NT;
+	uint4 gbuf[LOADS];
+#pragma unroll
+	for (int r = 0; r < LOADS; r++) {
+		const int u = tid + r * NT;
 		const int q = u / (8 * L), j = u % (8 * L);
-		const uint4 g = *(const uint4*)(src + block_idx(q) * L + 4 * j);
+		gbuf[r] = ld_stream(src + (outer_off | tile_off(q)) * L + 4 * j);
+	}
+#pragma unroll
+	for (int r = 0; r < LOADS; r++) {
+		const int u = tid + r * NT;
+		const int q = u / (8 * L), j = u % (8 * L);
+		const uint4 g = gbuf[r];
 		uint32_t* b = lds + q * BLK_WORDS;
-		if (ps.in_compact) {
+		if (IN_COMPACT) {
 			const uint32_t w[4] = {g.x, g.y, g.z, g.w};
 #pragma unroll
 			for (int t = 0; t < 4; t++) {
@@ -140,7 +173,7 @@ __global__ __launch_bounds__(128 * L) void antt_bs_pass(BsParams P) {
 		}
 	}
 	__syncthreads();
-	if (ps.in_compact) {
+	if (IN_COMPACT) {
 		for (int u = tid; u < kTileBlocks * L; u += NT) {
 			uint32_t* x = lds + (u / L) * BLK_WORDS + (u % L) * kLimbStride;
 			uint32_t r[32];
@@ -158,75 +191,96 @@ __global__ __launch_bounds__(128 * L) void antt_bs_pass(BsParams P) {
 		const int s = ps.lo + j;
 		const uint32_t* srow = P.s + (size_t)s * P.width;
 		const int nbits = P.log_h + P.log_rate - 1 - s;
+		// workgroup-uniform twiddle part: coset bits and the fixed (outer) index bits above s
+		const uint64_t ind_u = ((uint64_t)coset << (P.log_h - 1 - s)) | (uint64_t)(outer_off >> (s + 1));
+		uint32_t cu = 0;
+		for (int kk = 0; kk < nbits; kk++) cu ^= srow[kk] & (0u - (uint32_t)((ind_u >> kk) & 1));
+		// per-thread part: tile block bits above s (branch-free; srow[kk] is a uniform load)
+		auto tile_tw = [&](int q) -> uint32_t {
+			uint32_t w = 0;
+#pragma unroll
+			for (int m = 0; m < kBlkBits; m++) {
+				const int kk = ps.bb[m] - s - 1;
+				if (kk >= 0) w ^= srow[kk] & (0u - (uint32_t)((q >> m) & 1));
+			}
+			return w;
+		};
 		if (s >= 5) {
-			// block-bit stage: one thread per (block pair, limb)
+			// block-bit stage: one thread per (block pair, limb). Only V and the twiddle are live
+			// during the multiply; U is read afterwards.
 			const int m = ps.stage_m[j];
 			const int pair = tid / L, l = tid % L;
 			const int qu = ((pair >> m) << (m + 1)) | (pair & ((1 << m) - 1));
 			const int qv = qu | (1 << m);
-			const uint64_t ind = ((uint64_t)coset << (P.log_h - 1 - s)) | (uint64_t)(block_idx(qu) >> (s + 1));
-			uint32_t w = 0;
-			for (int kk = 0; kk < nbits; kk++) w ^= ((ind >> kk) & 1) ? srow[kk] : 0u;
-			uint32_t W[32], U[32], V[32];
+			const uint32_t w = cu ^ tile_tw(qu);
+			uint32_t W[32], V[32], Pr[32];
 #pragma unroll
 			for (int i = 0; i < 32; i++) W[i] = 0u - ((w >> i) & 1u);
 			uint32_t* pu = lds + qu * BLK_WORDS + l * kLimbStride;
 			uint32_t* pv = lds + qv * BLK_WORDS + l * kLimbStride;
 #pragma unroll
-			for (int i = 0; i < 32; i += 4) {
-				*(uint4*)(U + i) = *(const uint4*)(pu + i);
-				*(uint4*)(V + i) = *(const uint4*)(pv + i);
-			}
-			mul_acc_tw(V, W, U);
-#pragma unroll
-			for (int i = 0; i < 32; i++) V[i] ^= U[i];
+			for (int i = 0; i < 32; i += 4) *(uint4*)(V + i) = *(const uint4*)(pv + i);
+			mul_tw(V, W, Pr);
 #pragma unroll
 			for (int i = 0; i < 32; i += 4) {
-				*(uint4*)(pu + i) = *(const uint4*)(U + i);
-				*(uint4*)(pv + i) = *(const uint4*)(V + i);
+				uint4 u = *(const uint4*)(pu + i);
+				u.x ^= Pr[i];
+				u.y ^= Pr[i + 1];
+				u.z ^= Pr[i + 2];
+				u.w ^= Pr[i + 3];
+				*(uint4*)(pu + i) = u;
+				*(uint4*)(pv + i) = make_uint4(V[i] ^ u.x, V[i + 1] ^ u.y, V[i + 2] ^ u.z, V[i + 3] ^ u.w);
 			}
 		} else {
-			// intra-word stage: pairs are bit-lanes p, p + 2^s of the same word
+			// intra-word stage: pairs are bit-lanes p, p + 2^s of one word. Two blocks A, B are
+			// packed into one multiply: A's v-lanes move down onto the u positions, B's v-lanes
+			// stay on the v positions (the twiddle of a pair depends only on bits above s).
 			const int d = 1 << s;
 			const uint32_t um = ~lane_mask(s);
-			// twiddle of bit-lane p: sum_k blk_k srow[k], blk = (block_base + p) >> (s+1);
-			// blk bits below 4-s come from p (bit-lane patterns), the rest from the block.
-			uint32_t pat[32];
+			const int pair = tid / L, l = tid % L;
+			const int qa = pair, qb = pair | (kTileBlocks / 2);
+			const uint32_t ca = cu ^ tile_tw(qa), cb = cu ^ tile_tw(qb);
+			uint32_t W[32], T[32];
+			// bit-lane pattern part (uniform): bits s+1..4 of the lane index
 #pragma unroll
-			for (int i = 0; i < 32; i++) pat[i] = 0;
+			for (int i = 0; i < 32; i++) W[i] = ((0u - ((ca >> i) & 1u)) & um) ^ ((0u - ((cb >> i) & 1u)) & ~um);
 			for (int kk = 0; kk < 4 - s; kk++) {
 				const uint32_t t = srow[kk], mk = lane_mask(s + 1 + kk);
 #pragma unroll
-				for (int i = 0; i < 32; i++) pat[i] ^= ((t >> i) & 1u) ? mk : 0u;
+				for (int i = 0; i < 32; i++) W[i] ^= mk & (0u - ((t >> i) & 1u));
 			}
-			for (int u = tid; u < kTileBlocks * L; u += NT) {
-				const int q = u / L, l = u % L;
-				const uint64_t ind = ((uint64_t)coset << (P.log_h - 1 - s)) | (uint64_t)(block_idx(q) >> (s + 1));
-				uint32_t c = 0;
-				for (int kk = 4 - s; kk < nbits; kk++) c ^= ((ind >> kk) & 1) ? srow[kk] : 0u;
-				uint32_t W[32], X[32], T[32];
+			uint32_t* pa = lds + qa * BLK_WORDS + l * kLimbStride;
+			uint32_t* pb = lds + qb * BLK_WORDS + l * kLimbStride;
 #pragma unroll
-				for (int i = 0; i < 32; i++) W[i] = pat[i] ^ (0u - ((c >> i) & 1u));
-				uint32_t* px = lds + q * BLK_WORDS + l * kLimbStride;
+			for (int i = 0; i < 32; i += 4) {
+				const uint4 a = *(const uint4*)(pa + i), b = *(const uint4*)(pb + i);
+				T[i] = ((a.x >> d) & um) | (b.x & ~um);
+				T[i + 1] = ((a.y >> d) & um) | (b.y & ~um);
+				T[i + 2] = ((a.z >> d) & um) | (b.z & ~um);
+				T[i + 3] = ((a.w >> d) & um) | (b.w & ~um);
+			}
+			mul_tw(T, W, T);
 #pragma unroll
-				for (int i = 0; i < 32; i += 4) *(uint4*)(X + i) = *(const uint4*)(px + i);
+			for (int i = 0; i < 32; i += 4) {
+				uint32_t A[4], Bv[4];
+				*(uint4*)A = *(const uint4*)(pa + i);
+				*(uint4*)Bv = *(const uint4*)(pb + i);
 #pragma unroll
-				for (int i = 0; i < 32; i++) T[i] = X[i] >> d;
-				mul_tw(T, W, T);
-#pragma unroll
-				for (int i = 0; i < 32; i++) {
-					X[i] ^= T[i] & um;
-					X[i] ^= (X[i] & um) << d;
+				for (int t = 0; t < 4; t++) {
+					A[t] ^= T[i + t] & um;
+					Bv[t] ^= (T[i + t] & ~um) >> d;
+					A[t] ^= (A[t] & um) << d;
+					Bv[t] ^= (Bv[t] & um) << d;
 				}
-#pragma unroll
-				for (int i = 0; i < 32; i += 4) *(uint4*)(px + i) = *(const uint4*)(X + i);
+				*(uint4*)(pa + i) = *(const uint4*)A;
+				*(uint4*)(pb + i) = *(const uint4*)Bv;
 			}
 		}
 		__syncthreads();
 	}
 
 	// ---- store tile
-	if (ps.out_compact) {
+	if (OUT_COMPACT) {
 		for (int u = tid; u < kTileBlocks * L; u += NT) {
 			uint32_t* x = lds + (u / L) * BLK_WORDS + (u % L) * kLimbStride;
 			uint32_t r[32];
@@ -242,7 +296,7 @@ __global__ __launch_bounds__(128 * L) void antt_bs_pass(BsParams P) {
 		const int q = u / (8 * L), j = u % (8 * L);
 		const uint32_t* b = lds + q * BLK_WORDS;
 		uint4 g;
-		if (ps.out_compact) {
+		if (OUT_COMPACT) {
 			uint32_t w[4];
 #pragma unroll
 			for (int t = 0; t < 4; t++) {
@@ -254,7 +308,7 @@ __global__ __launch_bounds__(128 * L) void antt_bs_pass(BsParams P) {
 			const int l = (4 * j) / 32, i = (4 * j) % 32;
 			g = *(const uint4*)(b + l * kLimbStride + i);
 		}
-		*(uint4*)(dst + block_idx(q) * L + 4 * j) = g;
+		st_stream(dst + (outer_off | tile_off(q)) * L + 4 * j, g);
 	}
 }
 
@@ -263,7 +317,6 @@ __global__ __launch_bounds__(128 * L) void antt_bs_pass(BsParams P) {
 // ------------------------------------------------------------------------------------
 static std::vector<BsPass> plan_passes(int log_h) {
 	std::vector<BsPass> passes;
-	// bottom pass: contiguous 2^13-element tiles, stages 0..12
 	auto make = [&](int lo, int k, bool bottom) {
 		BsPass p{};
 		p.lo = lo;
@@ -299,20 +352,31 @@ static std::vector<BsPass> plan_passes(int log_h) {
 	}
 	passes.push_back(make(0, kMinLogH, true));
 	for (size_t i = 0; i < passes.size(); i++) {
-		passes[i].first = i == 0;
-		passes[i].in_compact = i == 0;
-		passes[i].out_compact = i + 1 == passes.size();
+		const bool first = i == 0, last = i + 1 == passes.size();
+		passes[i].role = first && last ? ROLE_SINGLE : first ? ROLE_FIRST : last ? ROLE_LAST : ROLE_MID;
 	}
 	return passes;
 }
 
+template <int L>
+static const void* kernel_for(int role) {
+	switch (role) {
+		case ROLE_FIRST: return (const void*)antt_bs_pass<L, ROLE_FIRST>;
+		case ROLE_MID: return (const void*)antt_bs_pass<L, ROLE_MID>;
+		case ROLE_LAST: return (const void*)antt_bs_pass<L, ROLE_LAST>;
+		default: return (const void*)antt_bs_pass<L, ROLE_SINGLE>;
+	}
+}
+
+static size_t lds_bytes(int L) { return (size_t)kTileBlocks * L * kLimbStride * sizeof(uint32_t); }
+
 bool bs_supports(const bn_antt_plan* plan) { return plan->log_h >= kMinLogH; }
 
 int bs_prepare(bn_antt_plan* plan) {
-	const size_t lds4 = (size_t)kTileBlocks * 4 * kLimbStride * sizeof(uint32_t);
-	const size_t lds1 = (size_t)kTileBlocks * 1 * kLimbStride * sizeof(uint32_t);
-	BN_HIP(hipFuncSetAttribute((const void*)antt_bs_pass<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds4));
-	BN_HIP(hipFuncSetAttribute((const void*)antt_bs_pass<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
+	for (int role = 0; role < 4; role++) {
+		BN_HIP(hipFuncSetAttribute(kernel_for<4>(role), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(4)));
+		BN_HIP(hipFuncSetAttribute(kernel_for<1>(role), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(1)));
+	}
 	plan->variant = 1;
 	return BN_OK;
 }
@@ -336,14 +400,11 @@ int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t 
 		if (const char* e = getenv("BN_DEBUG_STOP_STAGE"))  // debug: run stages >= this only
 			prm.p.stop_j = std::max(0, std::min(prm.p.k, atoi(e) - prm.p.lo));
 		const size_t grid = (batch << plan->log_rate) << passes[i].n_outer;
-		const size_t lds = (size_t)kTileBlocks * L * kLimbStride * sizeof(uint32_t);
 		int rc = timing_begin(plan, (int)i, st);
 		if (rc != BN_OK) return rc;
-		if (L == 4)
-			hipLaunchKernelGGL(antt_bs_pass<4>, dim3((unsigned)grid), dim3(512), lds, st, prm);
-		else
-			hipLaunchKernelGGL(antt_bs_pass<1>, dim3((unsigned)grid), dim3(128), lds, st, prm);
-		BN_HIP(hipGetLastError());
+		void* args[] = {&prm};
+		const void* fn = L == 4 ? kernel_for<4>(passes[i].role) : kernel_for<1>(passes[i].role);
+		BN_HIP(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(64 * L), args, lds_bytes(L), st));
 		rc = timing_end(plan, (int)i, st);
 		if (rc != BN_OK) return rc;
 	}
