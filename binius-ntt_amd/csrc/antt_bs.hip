@@ -14,12 +14,16 @@
 // Arithmetic
 //   Every twiddle lies in GF(2^32) and multiplies each GF(2^32) limb separately, so a
 //   GF(2^128) butterfly is four GF(2^32) bitsliced butterflies sharing one twiddle. Products
-//   use the generated Karatsuba circuits (bitsliced_gen.hpp, v_bitop3-fused); when every
-//   twiddle a wave needs lies in GF(2^8) or GF(2^16) the cheaper sub-field circuits are used
+//   use the generated Karatsuba circuits (bitsliced_gen.hpp, v_bitop3-fused); the host picks,
+//   per stage, the smallest sub-field (GF(2^8)/GF(2^16)/GF(2^32)) that holds every twiddle
 //   (multiplication by a sub-field scalar acts on each sub-field coordinate independently).
-//   Twiddles are linear in the block index (calculate_twiddle, additive_ntt.cuh:59-77), so
-//   the workgroup-uniform part (coset + fixed index bits) and the per-thread part (tile bits)
-//   are summed separately.
+//   Twiddles are linear in the butterfly-block index (calculate_twiddle, additive_ntt.cuh:
+//   59-77): the host tabulates, per stage, the contribution of every tile bit, every fixed
+//   (workgroup) index bit and every coset bit, so a twiddle is a handful of masked XORs.
+//
+// Stage schedule: block-bit stages go through LDS (partners change every stage). In the bottom
+// pass the 5 stages on index bits 0..4 pair bit-lanes of one word, so each thread keeps its two
+// blocks in registers for all of them and transposes them back to compact form in registers.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -34,24 +38,31 @@ constexpr int kBlkBits = 7;
 constexpr int kTileBlocks = 1 << kBlkBits;
 constexpr int kLimbStride = 36;  // LDS words per (block, limb): 32 + 4 pad (bank spread)
 constexpr int kMinLogH = kBlkBits + 5;
+constexpr int kMaxStages = kBlkBits + 5;  // stages per pass
+constexpr int kMaxOuter = 32 - 5 - kBlkBits;
+constexpr int kMaxRateBits = 8;
 
 enum { ROLE_FIRST = 0, ROLE_MID = 1, ROLE_LAST = 2, ROLE_SINGLE = 3 };
 
+// One pass = k consecutive stages lo..lo+k-1 over every tile. Passed by value as a kernel
+// argument (~2.6 KB), so every table read is a scalar load from the kernarg segment.
 struct BsPass {
-	int lo, k;
-	int bb[kBlkBits];  // index bit of tile block bit m
-	int stage_m[32];   // block bit m of stage (lo + j), j < k, for stages >= 5
-	int ob[32];        // outer index bits, ascending
-	int n_outer;
-	int stop_j;        // debug: lowest local stage processed (normally 0)
-	int role;
+	int lo, k, role, n_outer, stop_j;
+	int bb[kBlkBits];                        // index bit of tile block bit m
+	int ob[kMaxOuter];                       // fixed (outer) index bits, ascending
+	int stage_m[kMaxStages];                 // tile bit of stage lo + j (stages >= 5)
+	int field[kMaxStages];                   // 8/16/32: sub-field holding every twiddle of the stage
+	uint32_t twt[kMaxStages][kBlkBits];      // twiddle contribution of tile block bit m
+	uint32_t two[kMaxStages][kMaxOuter];     // ... of outer bit m
+	uint32_t twc[kMaxStages][kMaxRateBits];  // ... of coset bit c
+	uint32_t pat[5][32];                     // stages 0..4: bit-lane part of the twiddle words
 };
 
 struct BsParams {
 	const uint32_t* src;
 	uint32_t* dst;
-	const uint32_t* s;
-	int width, log_h, log_rate;
+	int log_h, log_rate;
+	int dbg;  // timing experiments only (BN_DEBUG_FLAGS): 1 no loads, 2 no stores, 4 no multiplies
 	BsPass p;
 };
 
@@ -71,46 +82,19 @@ __device__ __forceinline__ void st_stream(uint32_t* p, uint4 g) {
 }
 
 // bit masks of the bit-lanes p with bit j of p set
-__device__ __forceinline__ uint32_t lane_mask(int j) {
+__host__ __device__ constexpr uint32_t lane_mask(int j) {
 	return j == 0 ? 0xAAAAAAAAu : j == 1 ? 0xCCCCCCCCu : j == 2 ? 0xF0F0F0F0u : j == 3 ? 0xFF00FF00u : 0xFFFF0000u;
 }
 
-// u ^= w*v for 32 bitsliced GF(2^32) limbs, twiddle words W (bit i of the twiddle per lane),
-// choosing the smallest sub-field circuit that holds every twiddle of this wave.
-__device__ __forceinline__ void mul_acc_tw(const uint32_t* v, const uint32_t* W, uint32_t* u) {
-	uint32_t hi16 = 0, hi8 = 0;
+// out = w*x for 32 bitsliced GF(2^32) limbs (alias-safe: out may be x). W holds bit i of each
+// lane's twiddle in word i; `field` (uniform per stage) selects the sub-field circuit.
+__device__ __forceinline__ void mul_tw(int field, const uint32_t* x, const uint32_t* W, uint32_t* out) {
+	if (field <= 8) {
 #pragma unroll
-	for (int i = 16; i < 32; i++) hi16 |= W[i];
+		for (int g = 0; g < 4; g++) bsm3_mul(x + 8 * g, W, out + 8 * g);
+	} else if (field <= 16) {
 #pragma unroll
-	for (int i = 8; i < 16; i++) hi8 |= W[i];
-	if (!__any(hi16 != 0)) {
-		if (!__any(hi8 != 0)) {
-#pragma unroll
-			for (int g = 0; g < 4; g++) bsm3_mul_acc(v + 8 * g, W, u + 8 * g);
-		} else {
-#pragma unroll
-			for (int g = 0; g < 2; g++) bsm4_mul_acc(v + 16 * g, W, u + 16 * g);
-		}
-	} else {
-		bsm5_mul_acc(v, W, u);
-	}
-}
-
-// out = w*x (alias-safe: out may be x), same sub-field dispatch as mul_acc_tw.
-__device__ __forceinline__ void mul_tw(const uint32_t* x, const uint32_t* W, uint32_t* out) {
-	uint32_t hi16 = 0, hi8 = 0;
-#pragma unroll
-	for (int i = 16; i < 32; i++) hi16 |= W[i];
-#pragma unroll
-	for (int i = 8; i < 16; i++) hi8 |= W[i];
-	if (!__any(hi16 != 0)) {
-		if (!__any(hi8 != 0)) {
-#pragma unroll
-			for (int g = 0; g < 4; g++) bsm3_mul(x + 8 * g, W, out + 8 * g);
-		} else {
-#pragma unroll
-			for (int g = 0; g < 2; g++) bsm4_mul(x + 16 * g, W, out + 16 * g);
-		}
+		for (int g = 0; g < 2; g++) bsm4_mul(x + 16 * g, W, out + 16 * g);
 	} else {
 		bsm5_mul(x, W, out);
 	}
@@ -122,7 +106,8 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 	constexpr int BLK_WORDS = L * kLimbStride;
 	constexpr int NT = 64 * L;
 	constexpr bool IN_COMPACT = ROLE == ROLE_FIRST || ROLE == ROLE_SINGLE;
-	constexpr bool OUT_COMPACT = ROLE == ROLE_LAST || ROLE == ROLE_SINGLE;
+	constexpr bool LAST = ROLE == ROLE_LAST || ROLE == ROLE_SINGLE;  // bottom pass, compact out
+	uint32_t* cu_lds = lds + kTileBlocks * BLK_WORDS;                // workgroup part of each twiddle
 	const BsPass& ps = P.p;
 	const int tid = threadIdx.x;
 	const size_t n = (size_t)1 << P.log_h;
@@ -152,7 +137,17 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 	for (int r = 0; r < LOADS; r++) {
 		const int u = tid + r * NT;
 		const int q = u / (8 * L), j = u % (8 * L);
-		gbuf[r] = ld_stream(src + (outer_off | tile_off(q)) * L + 4 * j);
+		if (P.dbg & 1)
+			gbuf[r] = make_uint4(u, j, q, tid);
+		else
+			gbuf[r] = ld_stream(src + (outer_off | tile_off(q)) * L + 4 * j);
+	}
+	// workgroup-uniform twiddle part of every stage (outer + coset bits), one lane per stage
+	if (tid < ps.k) {
+		uint32_t c = 0;
+		for (int m = 0; m < ps.n_outer; m++) c ^= ps.two[tid][m] & (0u - (uint32_t)((outer >> m) & 1));
+		for (int b = 0; b < P.log_rate; b++) c ^= ps.twc[tid][b] & (0u - (uint32_t)((coset >> b) & 1));
+		cu_lds[tid] = c;
 	}
 #pragma unroll
 	for (int r = 0; r < LOADS; r++) {
@@ -186,103 +181,104 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 		__syncthreads();
 	}
 
-	// ---- stages, high to low
-	for (int j = ps.k - 1; j >= ps.stop_j; j--) {
-		const int s = ps.lo + j;
-		const uint32_t* srow = P.s + (size_t)s * P.width;
-		const int nbits = P.log_h + P.log_rate - 1 - s;
-		// workgroup-uniform twiddle part: coset bits and the fixed (outer) index bits above s
-		const uint64_t ind_u = ((uint64_t)coset << (P.log_h - 1 - s)) | (uint64_t)(outer_off >> (s + 1));
-		uint32_t cu = 0;
-		for (int kk = 0; kk < nbits; kk++) cu ^= srow[kk] & (0u - (uint32_t)((ind_u >> kk) & 1));
-		// per-thread part: tile block bits above s (branch-free; srow[kk] is a uniform load)
-		auto tile_tw = [&](int q) -> uint32_t {
-			uint32_t w = 0;
+	const int l = tid % L;
+	auto tile_tw = [&](int j, int q) -> uint32_t {
+		uint32_t w = 0;
 #pragma unroll
-			for (int m = 0; m < kBlkBits; m++) {
-				const int kk = ps.bb[m] - s - 1;
-				if (kk >= 0) w ^= srow[kk] & (0u - (uint32_t)((q >> m) & 1));
-			}
-			return w;
-		};
-		if (s >= 5) {
-			// block-bit stage: one thread per (block pair, limb). Only V and the twiddle are live
-			// during the multiply; U is read afterwards.
-			const int m = ps.stage_m[j];
-			const int pair = tid / L, l = tid % L;
-			const int qu = ((pair >> m) << (m + 1)) | (pair & ((1 << m) - 1));
-			const int qv = qu | (1 << m);
-			const uint32_t w = cu ^ tile_tw(qu);
-			uint32_t W[32], V[32], Pr[32];
+		for (int m = 0; m < kBlkBits; m++) w ^= ps.twt[j][m] & (0u - (uint32_t)((q >> m) & 1));
+		return w;
+	};
+
+	// ---- tile-bit stages (index bits >= 5), high to low, through LDS. One thread per
+	// (block pair, limb); only V and the twiddle are live during the multiply. Consecutive lanes
+	// take consecutive pairs, which keeps the padded LDS rows free of bank conflicts.
+	auto block_stage = [&](int j, int pair) {
+		const int m = ps.stage_m[j];
+		const int qu = ((pair >> m) << (m + 1)) | (pair & ((1 << m) - 1));
+		const int qv = qu | (1 << m);
+		const uint32_t w = cu_lds[j] ^ tile_tw(j, qu);
+		uint32_t W[32], V[32], Pr[32];
 #pragma unroll
-			for (int i = 0; i < 32; i++) W[i] = 0u - ((w >> i) & 1u);
-			uint32_t* pu = lds + qu * BLK_WORDS + l * kLimbStride;
-			uint32_t* pv = lds + qv * BLK_WORDS + l * kLimbStride;
+		for (int i = 0; i < 32; i++) W[i] = 0u - ((w >> i) & 1u);
+		uint32_t* pu = lds + qu * BLK_WORDS + l * kLimbStride;
+		uint32_t* pv = lds + qv * BLK_WORDS + l * kLimbStride;
 #pragma unroll
-			for (int i = 0; i < 32; i += 4) *(uint4*)(V + i) = *(const uint4*)(pv + i);
-			mul_tw(V, W, Pr);
+		for (int i = 0; i < 32; i += 4) *(uint4*)(V + i) = *(const uint4*)(pv + i);
+		if (P.dbg & 4) {
 #pragma unroll
-			for (int i = 0; i < 32; i += 4) {
-				uint4 u = *(const uint4*)(pu + i);
-				u.x ^= Pr[i];
-				u.y ^= Pr[i + 1];
-				u.z ^= Pr[i + 2];
-				u.w ^= Pr[i + 3];
-				*(uint4*)(pu + i) = u;
-				*(uint4*)(pv + i) = make_uint4(V[i] ^ u.x, V[i + 1] ^ u.y, V[i + 2] ^ u.z, V[i + 3] ^ u.w);
-			}
+			for (int i = 0; i < 32; i++) Pr[i] = V[i] ^ W[i];
 		} else {
-			// intra-word stage: pairs are bit-lanes p, p + 2^s of one word. Two blocks A, B are
-			// packed into one multiply: A's v-lanes move down onto the u positions, B's v-lanes
-			// stay on the v positions (the twiddle of a pair depends only on bits above s).
-			const int d = 1 << s;
-			const uint32_t um = ~lane_mask(s);
-			const int pair = tid / L, l = tid % L;
-			const int qa = pair, qb = pair | (kTileBlocks / 2);
-			const uint32_t ca = cu ^ tile_tw(qa), cb = cu ^ tile_tw(qb);
-			uint32_t W[32], T[32];
-			// bit-lane pattern part (uniform): bits s+1..4 of the lane index
-#pragma unroll
-			for (int i = 0; i < 32; i++) W[i] = ((0u - ((ca >> i) & 1u)) & um) ^ ((0u - ((cb >> i) & 1u)) & ~um);
-			for (int kk = 0; kk < 4 - s; kk++) {
-				const uint32_t t = srow[kk], mk = lane_mask(s + 1 + kk);
-#pragma unroll
-				for (int i = 0; i < 32; i++) W[i] ^= mk & (0u - ((t >> i) & 1u));
-			}
-			uint32_t* pa = lds + qa * BLK_WORDS + l * kLimbStride;
-			uint32_t* pb = lds + qb * BLK_WORDS + l * kLimbStride;
-#pragma unroll
-			for (int i = 0; i < 32; i += 4) {
-				const uint4 a = *(const uint4*)(pa + i), b = *(const uint4*)(pb + i);
-				T[i] = ((a.x >> d) & um) | (b.x & ~um);
-				T[i + 1] = ((a.y >> d) & um) | (b.y & ~um);
-				T[i + 2] = ((a.z >> d) & um) | (b.z & ~um);
-				T[i + 3] = ((a.w >> d) & um) | (b.w & ~um);
-			}
-			mul_tw(T, W, T);
-#pragma unroll
-			for (int i = 0; i < 32; i += 4) {
-				uint32_t A[4], Bv[4];
-				*(uint4*)A = *(const uint4*)(pa + i);
-				*(uint4*)Bv = *(const uint4*)(pb + i);
-#pragma unroll
-				for (int t = 0; t < 4; t++) {
-					A[t] ^= T[i + t] & um;
-					Bv[t] ^= (T[i + t] & ~um) >> d;
-					A[t] ^= (A[t] & um) << d;
-					Bv[t] ^= (Bv[t] & um) << d;
-				}
-				*(uint4*)(pa + i) = *(const uint4*)A;
-				*(uint4*)(pb + i) = *(const uint4*)Bv;
-			}
+			mul_tw(ps.field[j], V, W, Pr);  // sub-field circuits reuse W: Pr must not alias it
 		}
+#pragma unroll
+		for (int i = 0; i < 32; i += 4) {
+			uint4 u = *(const uint4*)(pu + i);
+			u.x ^= Pr[i];
+			u.y ^= Pr[i + 1];
+			u.z ^= Pr[i + 2];
+			u.w ^= Pr[i + 3];
+			*(uint4*)(pu + i) = u;
+			*(uint4*)(pv + i) = make_uint4(V[i] ^ u.x, V[i + 1] ^ u.y, V[i + 2] ^ u.z, V[i + 3] ^ u.w);
+		}
+	};
+	const int jlow = max(LAST ? 5 : 0, ps.stop_j);
+	for (int j = ps.k - 1; j >= jlow; j--) {
+		block_stage(j, tid / L);
 		__syncthreads();
 	}
 
-	// ---- store tile
-	if (OUT_COMPACT) {
-		for (int u = tid; u < kTileBlocks * L; u += NT) {
-			uint32_t* x = lds + (u / L) * BLK_WORDS + (u % L) * kLimbStride;
+	if (LAST) {
+		// ---- stages 4..0 (index bits inside the word), thread-private: thread (pair, limb)
+		// owns blocks qa = pair and qb = pair + 64 for all of them, so no barriers. Per stage
+		// both blocks share one multiply: A's v-lanes move down onto the u positions, B's
+		// v-lanes stay on the v positions (a pair's twiddle depends only on index bits above s).
+		const int qa = tid / L, qb = qa | (kTileBlocks / 2);
+		uint32_t* pa = lds + qa * BLK_WORDS + l * kLimbStride;
+		uint32_t* pb = lds + qb * BLK_WORDS + l * kLimbStride;
+		for (int s = 4; s >= ps.stop_j; s--) {  // the bottom pass starts at stage 0: j == s
+			{
+				const int d = 1 << s;
+				const uint32_t um = ~lane_mask(s);
+				const uint32_t ca = cu_lds[s] ^ tile_tw(s, qa), cb = cu_lds[s] ^ tile_tw(s, qb);
+				uint32_t W[32], T[32];
+#pragma unroll
+				for (int i = 0; i < 32; i += 4) {
+					const uint4 a = *(const uint4*)(pa + i), b = *(const uint4*)(pb + i);
+					T[i] = ((a.x >> d) & um) | (b.x & ~um);
+					T[i + 1] = ((a.y >> d) & um) | (b.y & ~um);
+					T[i + 2] = ((a.z >> d) & um) | (b.z & ~um);
+					T[i + 3] = ((a.w >> d) & um) | (b.w & ~um);
+				}
+#pragma unroll
+				for (int i = 0; i < 32; i++)
+					W[i] = ps.pat[s][i] ^ ((0u - ((ca >> i) & 1u)) & um) ^ ((0u - ((cb >> i) & 1u)) & ~um);
+				if (P.dbg & 4) {
+#pragma unroll
+					for (int i = 0; i < 32; i++) T[i] ^= W[i];
+				} else {
+					mul_tw(ps.field[s], T, W, T);
+				}
+#pragma unroll
+				for (int i = 0; i < 32; i += 4) {
+					uint32_t A[4], Bv[4];
+					*(uint4*)A = *(const uint4*)(pa + i);
+					*(uint4*)Bv = *(const uint4*)(pb + i);
+#pragma unroll
+					for (int t = 0; t < 4; t++) {
+						A[t] ^= T[i + t] & um;
+						Bv[t] ^= (T[i + t] & ~um) >> d;
+						A[t] ^= (A[t] & um) << d;
+						Bv[t] ^= (Bv[t] & um) << d;
+					}
+					*(uint4*)(pa + i) = *(const uint4*)A;
+					*(uint4*)(pb + i) = *(const uint4*)Bv;
+				}
+			}
+		}
+		// back to compact (limb-split) words, still thread-private
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			uint32_t* x = h ? pb : pa;
 			uint32_t r[32];
 #pragma unroll
 			for (int i = 0; i < 32; i += 4) *(uint4*)(r + i) = *(const uint4*)(x + i);
@@ -290,13 +286,15 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 #pragma unroll
 			for (int i = 0; i < 32; i += 4) *(uint4*)(x + i) = *(const uint4*)(r + i);
 		}
-		__syncthreads();
 	}
+	__syncthreads();
+
+	// ---- store tile
 	for (int u = tid; u < kTileBlocks * 8 * L; u += NT) {
 		const int q = u / (8 * L), j = u % (8 * L);
 		const uint32_t* b = lds + q * BLK_WORDS;
 		uint4 g;
-		if (OUT_COMPACT) {
+		if (LAST) {
 			uint32_t w[4];
 #pragma unroll
 			for (int t = 0; t < 4; t++) {
@@ -305,17 +303,23 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 			}
 			g = make_uint4(w[0], w[1], w[2], w[3]);
 		} else {
-			const int l = (4 * j) / 32, i = (4 * j) % 32;
-			g = *(const uint4*)(b + l * kLimbStride + i);
+			const int li = (4 * j) / 32, i = (4 * j) % 32;
+			g = *(const uint4*)(b + li * kLimbStride + i);
 		}
-		st_stream(dst + (outer_off | tile_off(q)) * L + 4 * j, g);
+		if (!(P.dbg & 2)) st_stream(dst + (outer_off | tile_off(q)) * L + 4 * j, g);
 	}
 }
 
 // ------------------------------------------------------------------------------------
 // host: pass planning
 // ------------------------------------------------------------------------------------
-static std::vector<BsPass> plan_passes(int log_h) {
+static std::vector<BsPass> plan_passes(const bn_antt_plan* plan) {
+	const int log_h = plan->log_h;
+	const int width = plan->width;
+	auto S = [&](int s, int kk) -> uint32_t {  // s[s][kk], 0 outside the table
+		if (kk < 0 || kk >= width - s) return 0u;
+		return plan->s_host[(size_t)s * width + kk];
+	};
 	std::vector<BsPass> passes;
 	auto make = [&](int lo, int k, bool bottom) {
 		BsPass p{};
@@ -330,14 +334,33 @@ static std::vector<BsPass> plan_passes(int log_h) {
 			for (int b = lo; b < lo + k; b++) bits.push_back(b);
 		}
 		for (int m = 0; m < kBlkBits; m++) p.bb[m] = bits[m];
-		for (int j = 0; j < k; j++) {
-			p.stage_m[j] = -1;
-			for (int m = 0; m < kBlkBits; m++)
-				if (p.bb[m] == lo + j) p.stage_m[j] = m;
-		}
 		p.n_outer = 0;
 		for (int b = 5; b < log_h; b++)
 			if (std::find(bits.begin(), bits.end(), b) == bits.end()) p.ob[p.n_outer++] = b;
+		for (int j = 0; j < k; j++) {
+			const int s = lo + j;
+			// twiddle of a butterfly block = XOR of s[s][kk] over the set bits kk of
+			// (coset << (log_h-1-s)) | (index >> (s+1)); index bit b contributes s[s][b-s-1]
+			uint32_t acc = 0;
+			for (int kk = 0; kk < width - s; kk++) acc |= S(s, kk);
+			p.field[j] = acc < 256u ? 8 : acc < 65536u ? 16 : 32;
+			p.stage_m[j] = -1;
+			for (int m = 0; m < kBlkBits; m++) {
+				if (p.bb[m] == s) p.stage_m[j] = m;
+				p.twt[j][m] = S(s, p.bb[m] - s - 1);
+			}
+			for (int m = 0; m < p.n_outer; m++) p.two[j][m] = S(s, p.ob[m] - s - 1);
+			for (int c = 0; c < plan->log_rate; c++) p.twc[j][c] = S(s, log_h - 1 - s + c);
+			if (s < 5) {
+				// bit-lane p of a word has index bits 0..4 = p: bits s+1..4 contribute per lane
+				for (int i = 0; i < 32; i++) {
+					uint32_t w = 0;
+					for (int b = s + 1; b < 5; b++)
+						if ((S(s, b - s - 1) >> i) & 1) w ^= lane_mask(b);
+					p.pat[s][i] = w;
+				}
+			}
+		}
 		return p;
 	};
 	const int rest = log_h - kMinLogH;
@@ -368,9 +391,12 @@ static const void* kernel_for(int role) {
 	}
 }
 
-static size_t lds_bytes(int L) { return (size_t)kTileBlocks * L * kLimbStride * sizeof(uint32_t); }
+// tile + one word per stage for the workgroup-uniform twiddle parts
+static size_t lds_bytes(int L) { return ((size_t)kTileBlocks * L * kLimbStride + kMaxStages) * sizeof(uint32_t); }
 
-bool bs_supports(const bn_antt_plan* plan) { return plan->log_h >= kMinLogH; }
+bool bs_supports(const bn_antt_plan* plan) {
+	return plan->log_h >= kMinLogH && plan->log_h - 5 - kBlkBits <= kMaxOuter && plan->log_rate <= kMaxRateBits;
+}
 
 int bs_prepare(bn_antt_plan* plan) {
 	for (int role = 0; role < 4; role++) {
@@ -382,22 +408,23 @@ int bs_prepare(bn_antt_plan* plan) {
 }
 
 int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st) {
-	const auto passes = plan_passes(plan->log_h);
+	const auto passes = plan_passes(plan);
 	const int L = plan->limbs;
-	// debug hook: BN_DEBUG_MAX_PASSES=n runs only the first n passes
+	// debug hooks: BN_DEBUG_MAX_PASSES=n runs only the first n passes,
+	// BN_DEBUG_STOP_STAGE=s runs only stages >= s
 	size_t npass = passes.size();
 	if (const char* e = getenv("BN_DEBUG_MAX_PASSES")) npass = std::min(npass, (size_t)atoi(e));
 	for (size_t i = 0; i < npass; i++) {
 		BsParams prm;
 		prm.src = d_in;
 		prm.dst = d_out;
-		prm.s = plan->s_dev;
-		prm.width = plan->width;
 		prm.log_h = plan->log_h;
 		prm.log_rate = plan->log_rate;
+		prm.dbg = 0;
+		if (const char* e = getenv("BN_DEBUG_FLAGS")) prm.dbg = atoi(e);
 		prm.p = passes[i];
 		prm.p.stop_j = 0;
-		if (const char* e = getenv("BN_DEBUG_STOP_STAGE"))  // debug: run stages >= this only
+		if (const char* e = getenv("BN_DEBUG_STOP_STAGE"))
 			prm.p.stop_j = std::max(0, std::min(prm.p.k, atoi(e) - prm.p.lo));
 		const size_t grid = (batch << plan->log_rate) << passes[i].n_outer;
 		int rc = timing_begin(plan, (int)i, st);
