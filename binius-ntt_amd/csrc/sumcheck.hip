@@ -1,23 +1,601 @@
-// GF(2^128) sumcheck prover (placeholder until the bitsliced kernels land).
-#include "common.hpp"
+// GF(2^128) sumcheck prover on bitsliced columns (Sumcheck<N, d, T>, src/ulvt/sumcheck/sumcheck.cuh).
+//
+// Semantics (sumcheck.cuh:130-300, fold_batch / compute_sum in core/core.cu): with columns
+// f_0..f_{d-1} of cur evaluations and h = cur / 2,
+//   points[k] = sum_{x<h} prod_j (f_j(x) + k (f_j(x) + f_j(x+h))),  k = 0..d (tower element k)
+//   sum       = points[0] + points[1]   (= sum_{x<cur} prod_j f_j(x); for cur == 1: prod_j f_j(0))
+//   fold(r)   : f_j(x) <- f_j(x) + r (f_j(x) + f_j(x+h))   (highest variable first)
+//
+// Layout: each column is a run of bitsliced 128-word batches (32 elements; word i = bit i of
+// the 32 elements, element e in bit e), columns back to back. While cur >= 64 a butterfly pairs
+// whole batches x and x + cur/64; below that the single remaining batch pairs bit-lanes.
+//
+// Arithmetic: one GF(2^128) bitsliced product is spread over a quad of lanes (lane l holds limb
+// l = words 32l..32l+31 of each operand and of the result). With A = A_hi X + A_lo the tower's
+// top level is done schoolbook (as tower_height_7_mul, tower_7_mul.cu:4-20): lane q computes one
+// GF(2^64) product P_q = A_i B_j, (i,j) = (0,0), (1,1), (0,1), (1,0), by Karatsuba over three
+// generated GF(2^32) circuits (bsm5_mul); then
+//   c_lo = P00 + P11,  c_hi = P01 + P10 + alpha(P11)
+// and the quad trades halves through LDS. Operands and partial products travel through a
+// 1 KiB LDS slot per quad, so a lane never holds more than ~4 x 32 words of field data.
+//
+// Round messages are reduced without ever forming 128-word sums: after each product a lane
+// folds its 32 result words into one word of parities (bit i = XOR over the elements of bit i),
+// which is exactly the limb of the element-sum that the reference's compute_sum produces.
+#include <hip/hip_runtime.h>
+#include <string.h>
 
-struct bn_sumcheck {
-	int dummy;
+#include <vector>
+
+#include "bitsliced.hpp"
+#include "common.hpp"
+#include "tower.hpp"
+
+namespace bn {
+namespace {
+
+constexpr int kScThreads = 256;
+constexpr int kQuadsPerWG = kScThreads / 4;
+constexpr int kQuadWords = 256;  // LDS words per quad
+constexpr int kMaxD = 8;
+
+// compiler ordering for LDS traffic between lanes of one wave (the hardware executes a wave's
+// LDS instructions in order)
+__device__ __forceinline__ void wsync() {
+	asm volatile("" ::: "memory");
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void ld32(uint32_t* r, const uint32_t* p) {
+#pragma unroll
+	for (int i = 0; i < 32; i += 4) *(uint4*)(r + i) = *(const uint4*)(p + i);
+}
+__device__ __forceinline__ void st32(uint32_t* p, const uint32_t* r) {
+#pragma unroll
+	for (int i = 0; i < 32; i += 4) *(uint4*)(p + i) = *(const uint4*)(r + i);
+}
+
+// bitsliced multiply_alpha on GF(2^(2^H)) (binary_tower.cuh multiply_alpha): out may not alias a
+template <int H>
+__device__ __forceinline__ void bs_alpha(const uint32_t* a, uint32_t* out) {
+	if constexpr (H == 0) {
+		out[0] = a[0];
+	} else {
+		constexpr int half = 1 << (H - 1);
+		uint32_t t[half];
+		bs_alpha<H - 1>(a + half, t);
+#pragma unroll
+		for (int i = 0; i < half; i++) {
+			out[i] = a[half + i];
+			out[half + i] = a[i] ^ t[i];
+		}
+	}
+}
+
+// GF(2^128) product inside a quad's LDS slot S (256 words). On entry S[32l..32l+32) holds limb
+// l of the first operand and B[32l..32l+32) limb l of the second (B = S + 128, or a shared
+// broadcast operand elsewhere in LDS). On exit S[32l..32l+32) holds limb l of the product.
+__device__ __forceinline__ void quad_mul(uint32_t* S, const uint32_t* B, int l) {
+	wsync();
+	const int ia = l & 1, jb = (l == 1 || l == 2) ? 1 : 0;
+	const uint32_t* A0 = S + 64 * ia;
+	const uint32_t* B0 = B + 64 * jb;
+	uint32_t x[32], y[32], z[32];
+	// GF(2^64) Karatsuba: z0 = a0 b0, z2 = a1 b1, z1 = (a0+a1)(b0+b1) + z0 + z2; at most one
+	// 32-word value is live across a circuit (the circuits themselves need ~160 VGPRs), the
+	// rest is parked in the quad's LDS slot once the operands have been consumed.
+	ld32(x, A0);
+	ld32(y, B0);
+	bsm5_mul(x, y, z);  // z0
+	__builtin_amdgcn_sched_barrier(0);
+	ld32(x, A0 + 32);
+	ld32(y, B0 + 32);
+	bsm5_mul(x, y, y);  // z2
+	__builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+	for (int i = 0; i < 32; i++) z[i] ^= y[i];  // lo = z0 + z2
+	bs_alpha<5>(y, x);
+#pragma unroll
+	for (int i = 0; i < 32; i++) y[i] = z[i] ^ x[i];  // lo + alpha(z2)
+	uint32_t sa[32], sb[32];
+#pragma unroll
+	for (int i = 0; i < 32; i += 4) {
+		const uint4 p = *(const uint4*)(A0 + i), q = *(const uint4*)(A0 + 32 + i);
+		const uint4 u = *(const uint4*)(B0 + i), v = *(const uint4*)(B0 + 32 + i);
+		sa[i] = p.x ^ q.x, sa[i + 1] = p.y ^ q.y, sa[i + 2] = p.z ^ q.z, sa[i + 3] = p.w ^ q.w;
+		sb[i] = u.x ^ v.x, sb[i + 1] = u.y ^ v.y, sb[i + 2] = u.z ^ v.z, sb[i + 3] = u.w ^ v.w;
+	}
+	wsync();  // every lane of the quad has read its operands: the slot is free
+	st32(S + 64 * l, z);
+	st32(S + 64 * l + 32, y);
+	__builtin_amdgcn_sched_barrier(0);
+	bsm5_mul(sa, sb, x);  // (a0+a1)(b0+b1)
+	__builtin_amdgcn_sched_barrier(0);
+	ld32(y, S + 64 * l + 32);
+#pragma unroll
+	for (int i = 0; i < 32; i++) x[i] ^= y[i];  // hi = z1 + alpha(z2)
+	st32(S + 64 * l + 32, x);
+	wsync();
+	// lane l assembles limb l: limbs 0,1 = P00 + P11; limbs 2,3 = P01 + P10 + alpha64(P11),
+	// alpha64(P) = (P.hi, P.lo + alpha(P.hi))
+	const int p0 = l < 2 ? 0 : 2, half = l & 1;
+	const uint32_t m2 = (l == 2) ? ~0u : 0u, m3 = (l == 3) ? ~0u : 0u;
+	ld32(x, S + 64 * 1 + 32);  // P11.hi
+	bs_alpha<5>(x, y);
+#pragma unroll
+	for (int i = 0; i < 32; i++) {
+		const uint32_t e = S[64 * p0 + 32 * half + i] ^ S[64 * (p0 + 1) + 32 * half + i];
+		z[i] = e ^ (x[i] & m2) ^ ((S[64 + i] ^ y[i]) & m3);
+	}
+	wsync();
+	st32(S + 32 * l, z);
+	wsync();
+}
+
+// out = k * x for a tower constant k < 16 acting on the 8 GF(2^4) coordinates of a limb
+// (alias-safe)
+__device__ __forceinline__ void mul_small(uint32_t k, const uint32_t* x, uint32_t* out) {
+	uint32_t c[4];
+#pragma unroll
+	for (int a = 0; a < 4; a++) c[a] = (uint32_t)tw_mul(k, 1u << a, 2);
+#pragma unroll
+	for (int g = 0; g < 8; g++) {
+		uint32_t r[4];
+#pragma unroll
+		for (int b = 0; b < 4; b++) {
+			r[b] = 0;
+#pragma unroll
+			for (int a = 0; a < 4; a++) r[b] ^= x[4 * g + a] & (0u - ((c[a] >> b) & 1u));
+		}
+#pragma unroll
+		for (int b = 0; b < 4; b++) out[4 * g + b] = r[b];
+	}
+}
+
+// bit i = parity of (w[i] & mask): the limb of the sum over the batch's (masked) elements
+__device__ __forceinline__ uint32_t parity_word(const uint32_t* w, uint32_t mask) {
+	uint32_t r = 0;
+#pragma unroll
+	for (int i = 0; i < 32; i++) r |= (uint32_t)(__popc(w[i] & mask) & 1) << i;
+	return r;
+}
+
+struct ScArgs {
+	uint32_t* cols;
+	size_t col_stride;  // words between columns
+	int d;
+	size_t n_pairs;     // batch pairs (big mode) or 1 (small modes)
+	size_t hb;          // batch distance of a pair (big mode)
+	int h;              // element distance of a pair inside the batch (small modes)
+	int mode;           // 0 big, 1 in-batch pairs, 2 single element (cur == 1)
+	int kmax;           // points 0..kmax
+	uint32_t r[4];      // fold challenge
+	uint32_t* acc;      // (kmax + 1) x 4 words, XOR-accumulated
 };
 
-extern "C" int bn_sumcheck_create(int, int, int, int, const uint32_t*, bn_sumcheck** sc) {
-	if (sc) *sc = nullptr;
-	BN_FAIL(BN_ERR_UNSUPPORTED, "sumcheck not built yet");
+// lo/hi limbs of column j for pair p (this lane's limb l)
+template <int MODE>
+__device__ __forceinline__ void load_pair(const ScArgs& A, int j, size_t p, int l, uint32_t* lo, uint32_t* hi, uint32_t& emask) {
+	const uint32_t* c = A.cols + (size_t)j * A.col_stride;
+	if constexpr (MODE == 0) {
+		ld32(lo, c + 128 * p + 32 * l);
+		ld32(hi, c + 128 * (p + A.hb) + 32 * l);
+		emask = ~0u;
+	} else if constexpr (MODE == 1) {
+		const uint32_t m = (1u << A.h) - 1u;
+		uint32_t w[32];
+		ld32(w, c + 32 * l);
+#pragma unroll
+		for (int i = 0; i < 32; i++) {
+			lo[i] = w[i] & m;
+			hi[i] = (w[i] >> A.h) & m;
+		}
+		emask = m;
+	} else {
+		ld32(lo, c + 32 * l);
+#pragma unroll
+		for (int i = 0; i < 32; i++) {
+			lo[i] &= 1u;
+			hi[i] = lo[i];  // k = 0 only: f = lo
+		}
+		emask = 1u;
+	}
 }
-extern "C" int bn_sumcheck_create_device(int, int, int, int, void*, int, bn_sumcheck** sc) {
-	if (sc) *sc = nullptr;
-	BN_FAIL(BN_ERR_UNSUPPORTED, "sumcheck not built yet");
+
+template <int MODE>
+__global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
+	extern __shared__ uint32_t lds[];
+	const int l = threadIdx.x & 3, qw = threadIdx.x >> 2;
+	uint32_t* S = lds + qw * kQuadWords;
+	const size_t quad0 = (size_t)blockIdx.x * kQuadsPerWG + qw, nquads = (size_t)gridDim.x * kQuadsPerWG;
+	for (int k = 0; k <= A.kmax; k++) {
+		uint32_t acc = 0;
+		for (size_t p = quad0; p < A.n_pairs; p += nquads) {
+			uint32_t emask = 0;
+			for (int j = 0; j < A.d; j++) {
+				// f_j at point k: lo + k (lo + hi), written into the A (j == 0) or B operand
+				uint32_t lo[32], hi[32];
+				load_pair<MODE>(A, j, p, l, lo, hi, emask);
+				if (k == 0) {
+				} else if (k == 1) {
+#pragma unroll
+					for (int i = 0; i < 32; i++) lo[i] = hi[i];
+				} else {
+#pragma unroll
+					for (int i = 0; i < 32; i++) hi[i] ^= lo[i];
+					mul_small((uint32_t)k, hi, hi);
+#pragma unroll
+					for (int i = 0; i < 32; i++) lo[i] ^= hi[i];
+				}
+				st32(S + (j == 0 ? 0 : 128) + 32 * l, lo);
+				if (j > 0) quad_mul(S, S + 128, l);
+			}
+			wsync();
+			uint32_t t[32];
+			ld32(t, S + 32 * l);
+			acc ^= parity_word(t, emask);
+			wsync();
+		}
+		// XOR-reduce over the quads of the wave (lanes with the same limb), then one atomic per limb
+		acc ^= __shfl_xor(acc, 4);
+		acc ^= __shfl_xor(acc, 8);
+		acc ^= __shfl_xor(acc, 16);
+		acc ^= __shfl_xor(acc, 32);
+		if ((threadIdx.x & 63) < 4 && acc) atomicXor(A.acc + 4 * k + l, acc);
+	}
 }
-extern "C" int bn_sumcheck_round_messages(bn_sumcheck*, uint32_t*, uint32_t*) { BN_FAIL(BN_ERR_UNSUPPORTED, "sumcheck not built yet"); }
-extern "C" int bn_sumcheck_move_to_next_round(bn_sumcheck*, const uint32_t*) { BN_FAIL(BN_ERR_UNSUPPORTED, "sumcheck not built yet"); }
-extern "C" int bn_sumcheck_round(const bn_sumcheck*, int*) { BN_FAIL(BN_ERR_UNSUPPORTED, "sumcheck not built yet"); }
-extern "C" int bn_sumcheck_set_shard(bn_sumcheck*, int, int) { BN_FAIL(BN_ERR_UNSUPPORTED, "sumcheck not built yet"); }
-extern "C" int bn_sumcheck_destroy(bn_sumcheck* sc) {
+
+template <int MODE>
+__global__ __launch_bounds__(kScThreads, 2) void sc_fold(ScArgs A) {
+	extern __shared__ uint32_t lds[];
+	const int l = threadIdx.x & 3, qw = threadIdx.x >> 2;
+	uint32_t* S = lds + qw * kQuadWords;
+	uint32_t* R = lds + kQuadsPerWG * kQuadWords;  // the challenge, broadcast-bitsliced, shared
+	if (threadIdx.x < 128) R[threadIdx.x] = 0u - ((A.r[threadIdx.x / 32] >> (threadIdx.x % 32)) & 1u);
+	__syncthreads();
+	const size_t quad0 = (size_t)blockIdx.x * kQuadsPerWG + qw, nquads = (size_t)gridDim.x * kQuadsPerWG;
+	const size_t items = (size_t)A.d * A.n_pairs;
+	for (size_t it = quad0; it < items; it += nquads) {
+		const int j = (int)(it / A.n_pairs);
+		const size_t p = it % A.n_pairs;
+		uint32_t lo[32], hi[32], emask;
+		load_pair<MODE>(A, j, p, l, lo, hi, emask);
+#pragma unroll
+		for (int i = 0; i < 32; i++) hi[i] ^= lo[i];
+		st32(S + 32 * l, hi);
+		quad_mul(S, R, l);
+		// lo is re-read (cache-resident) rather than kept live across the product
+		load_pair<MODE>(A, j, p, l, lo, hi, emask);
+		ld32(hi, S + 32 * l);
+#pragma unroll
+		for (int i = 0; i < 32; i++) lo[i] = (lo[i] ^ hi[i]) & emask;
+		wsync();
+		st32(A.cols + (size_t)j * A.col_stride + 128 * p + 32 * l, lo);
+	}
+}
+
+size_t lds_bytes() { return ((size_t)kQuadsPerWG * kQuadWords + 128) * sizeof(uint32_t); }
+
+struct DeviceScope {
+	int prev = -1;
+	bool ok = true;
+	explicit DeviceScope(int dev) {
+		if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+		if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+	}
+	~DeviceScope() {
+		int cur = -1;
+		if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) hipSetDevice(prev);
+	}
+};
+
+}  // namespace
+}  // namespace bn
+
+struct bn_sumcheck {
+	int device = 0;
+	int num_vars = 0, d = 0;
+	int rank = 0, world = 1;
+	int round = 0;
+	size_t cur = 0;         // evaluations per column held by this prover
+	size_t col_words = 0;   // words between columns (allocation)
+	uint32_t* cols = nullptr;
+	uint32_t* acc = nullptr;
+	hipStream_t stream = nullptr;
+	bool sharded_used = false;
+};
+
+namespace {
+
+using namespace bn;
+
+int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
+	ScArgs A{};
+	A.cols = sc->cols;
+	A.col_stride = sc->col_words;
+	A.d = sc->d;
+	if (sc->cur >= 64) {
+		A.mode = 0;
+		A.n_pairs = sc->cur / 64;
+		A.hb = sc->cur / 64;
+		A.kmax = sc->d;
+	} else if (sc->cur >= 2) {
+		A.mode = 1;
+		A.n_pairs = 1;
+		A.h = (int)(sc->cur / 2);
+		A.kmax = sc->d;
+	} else {
+		A.mode = 2;
+		A.n_pairs = 1;
+		A.kmax = 0;
+	}
+	A.acc = sc->acc;
+	if (fold) memcpy(A.r, r, 16);
+	const size_t items = fold ? (size_t)sc->d * A.n_pairs : A.n_pairs;
+	size_t grid = (items + kQuadsPerWG - 1) / kQuadsPerWG;
+	if (grid > 4096) grid = 4096;
+	if (!fold) BN_HIP(hipMemsetAsync(sc->acc, 0, sizeof(uint32_t) * 4 * (kMaxD + 1), sc->stream));
+	void* args[] = {&A};
+	const void* fns[2][3] = {{(const void*)sc_messages<0>, (const void*)sc_messages<1>, (const void*)sc_messages<2>},
+							 {(const void*)sc_fold<0>, (const void*)sc_fold<1>, (const void*)sc_fold<2>}};
+	BN_HIP(hipLaunchKernel(fns[fold ? 1 : 0][A.mode], dim3((unsigned)grid), dim3(kScThreads),
+						   args, lds_bytes(), sc->stream));
+	return BN_OK;
+}
+
+int sc_alloc(bn_sumcheck* sc, size_t col_words) {
+	sc->col_words = col_words;
+	BN_HIP(hipMalloc(&sc->cols, sizeof(uint32_t) * col_words * (size_t)sc->d));
+	return BN_OK;
+}
+
+int sc_common_init(bn_sumcheck* sc) {
+	BN_HIP(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
+	BN_HIP(hipMalloc(&sc->acc, sizeof(uint32_t) * 4 * (kMaxD + 1)));
+	const void* fns[6] = {(const void*)sc_messages<0>, (const void*)sc_messages<1>, (const void*)sc_messages<2>,
+						  (const void*)sc_fold<0>,     (const void*)sc_fold<1>,     (const void*)sc_fold<2>};
+	for (const void* f : fns) BN_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes()));
+	return BN_OK;
+}
+
+void sc_free(bn_sumcheck* sc) {
+	if (!sc) return;
+	if (sc->stream) hipStreamSynchronize(sc->stream);
+	if (sc->cols) hipFree(sc->cols);
+	if (sc->acc) hipFree(sc->acc);
+	if (sc->stream) hipStreamDestroy(sc->stream);
 	delete sc;
+}
+
+int check_shape(int num_vars, int d, int transposed) {
+	BN_CHECK_ARG(d >= 1 && d <= kMaxD, "composition_size must be in [1, %d]", kMaxD);
+	BN_CHECK_ARG(num_vars >= 1 && num_vars <= 30, "num_vars must be in [1, 30]");
+	BN_CHECK_ARG(!transposed || num_vars >= 5, "bitsliced input needs num_vars >= 5 (whole 32-element batches)");
+	return BN_OK;
+}
+
+// Common tail of both constructors: `stage` holds the d columns back to back (4*2^n words
+// each, compact or bitsliced); it becomes the prover's storage (converted in place).
+int sc_finish_create(bn_sumcheck* sc, int transposed) {
+	const size_t n = (size_t)1 << sc->num_vars;
+	if (!transposed) {
+		const size_t blocks = sc->col_words / 128 * (size_t)sc->d;
+		int rc = bn_bitslice_device(sc->cols, blocks, 0, sc->stream);
+		if (rc != BN_OK) return rc;
+	}
+	sc->cur = n;
+	sc->round = 0;
+	BN_HIP(hipStreamSynchronize(sc->stream));
+	return BN_OK;
+}
+
+}  // namespace
+
+extern "C" int bn_sumcheck_create(int device, int num_vars, int d, int transposed, const uint32_t* evals,
+								  bn_sumcheck** out) {
+	BN_CHECK_ARG(out, "NULL output pointer");
+	*out = nullptr;
+	BN_CHECK_ARG(evals, "NULL evals");
+	int rc = check_shape(num_vars, d, transposed);
+	if (rc != BN_OK) return rc;
+	DeviceScope ds(device);
+	if (!ds.ok) BN_FAIL(BN_ERR_HIP, "hipSetDevice(%d) failed", device);
+	bn_sumcheck* sc = new bn_sumcheck;
+	sc->device = device;
+	sc->num_vars = num_vars;
+	sc->d = d;
+	const size_t n = (size_t)1 << num_vars;
+	const size_t in_words = 4 * n;
+	const size_t col_words = in_words < 128 ? 128 : in_words;  // pad to one batch
+	if ((rc = sc_common_init(sc)) != BN_OK || (rc = sc_alloc(sc, col_words)) != BN_OK) {
+		sc_free(sc);
+		return rc;
+	}
+	hipError_t e = hipSuccess;
+	if (col_words != in_words) e = hipMemsetAsync(sc->cols, 0, sizeof(uint32_t) * col_words * (size_t)d, sc->stream);
+	for (int j = 0; j < d && e == hipSuccess; j++)
+		e = hipMemcpyAsync(sc->cols + (size_t)j * col_words, evals + (size_t)j * in_words, sizeof(uint32_t) * in_words,
+						   hipMemcpyHostToDevice, sc->stream);
+	if (e != hipSuccess) {
+		sc_free(sc);
+		BN_FAIL(BN_ERR_HIP, "copying evals to the device: %s", hipGetErrorString(e));
+	}
+	if ((rc = sc_finish_create(sc, transposed)) != BN_OK) {
+		sc_free(sc);
+		return rc;
+	}
+	*out = sc;
+	return BN_OK;
+}
+
+extern "C" int bn_sumcheck_create_device(int device, int num_vars, int d, int transposed, void* d_evals, int take,
+										 bn_sumcheck** out) {
+	BN_CHECK_ARG(out, "NULL output pointer");
+	*out = nullptr;
+	BN_CHECK_ARG(d_evals, "NULL evals");
+	int rc = check_shape(num_vars, d, transposed);
+	if (rc != BN_OK) return rc;
+	DeviceScope ds(device);
+	if (!ds.ok) BN_FAIL(BN_ERR_HIP, "hipSetDevice(%d) failed", device);
+	bn_sumcheck* sc = new bn_sumcheck;
+	sc->device = device;
+	sc->num_vars = num_vars;
+	sc->d = d;
+	const size_t n = (size_t)1 << num_vars;
+	const size_t in_words = 4 * n;
+	if ((rc = sc_common_init(sc)) != BN_OK) {
+		sc_free(sc);
+		return rc;
+	}
+	if (take && in_words >= 128) {
+		sc->cols = (uint32_t*)d_evals;
+		sc->col_words = in_words;
+	} else {
+		const size_t col_words = in_words < 128 ? 128 : in_words;
+		if ((rc = sc_alloc(sc, col_words)) != BN_OK) {
+			sc_free(sc);
+			return rc;
+		}
+		hipError_t e = hipSuccess;
+		if (col_words != in_words) e = hipMemsetAsync(sc->cols, 0, sizeof(uint32_t) * col_words * (size_t)d, sc->stream);
+		for (int j = 0; j < d && e == hipSuccess; j++)
+			e = hipMemcpyAsync(sc->cols + (size_t)j * col_words, (const uint32_t*)d_evals + (size_t)j * in_words,
+							   sizeof(uint32_t) * in_words, hipMemcpyDeviceToDevice, sc->stream);
+		if (e == hipSuccess && take) e = hipStreamSynchronize(sc->stream);
+		if (e == hipSuccess && take) e = hipFree(d_evals);
+		if (e != hipSuccess) {
+			sc_free(sc);
+			BN_FAIL(BN_ERR_HIP, "copying device evals: %s", hipGetErrorString(e));
+		}
+	}
+	if ((rc = sc_finish_create(sc, transposed)) != BN_OK) {
+		sc_free(sc);
+		return rc;
+	}
+	*out = sc;
+	return BN_OK;
+}
+
+extern "C" int bn_sumcheck_set_shard(bn_sumcheck* sc, int rank, int world) {
+	BN_CHECK_ARG(sc, "NULL prover");
+	BN_CHECK_ARG(sc->round == 0 && !sc->sharded_used, "set_shard must precede the first round");
+	BN_CHECK_ARG(world >= 1 && (world & (world - 1)) == 0, "world must be a power of two");
+	BN_CHECK_ARG(rank >= 0 && rank < world, "rank out of range");
+	const size_t n = (size_t)1 << sc->num_vars;
+	BN_CHECK_ARG(n >= (size_t)32 * world, "need at least one 32-element batch per rank");
+	if (world == 1) return BN_OK;
+	DeviceScope ds(sc->device);
+	// keep the batches b with b mod world == rank, in order
+	const size_t nb_local = n / 32 / world;
+	uint32_t* local = nullptr;
+	BN_HIP(hipMalloc(&local, sizeof(uint32_t) * 128 * nb_local * (size_t)sc->d));
+	for (int j = 0; j < sc->d; j++)
+		BN_HIP(hipMemcpy2DAsync(local + (size_t)j * 128 * nb_local, 128 * sizeof(uint32_t),
+								sc->cols + (size_t)j * sc->col_words + 128 * (size_t)rank, 128 * sizeof(uint32_t) * world,
+								128 * sizeof(uint32_t), nb_local, hipMemcpyDeviceToDevice, sc->stream));
+	BN_HIP(hipStreamSynchronize(sc->stream));
+	BN_HIP(hipFree(sc->cols));
+	sc->cols = local;
+	sc->col_words = 128 * nb_local;
+	sc->cur = n / world;
+	sc->rank = rank;
+	sc->world = world;
+	sc->sharded_used = true;
+	return BN_OK;
+}
+
+extern "C" int bn_sumcheck_needs_gather(const bn_sumcheck* sc, int* flag) {
+	BN_CHECK_ARG(sc && flag, "NULL argument");
+	*flag = (sc->world > 1 && sc->cur <= 32) ? 1 : 0;
+	return BN_OK;
+}
+
+extern "C" int bn_sumcheck_export_shard(const bn_sumcheck* sc, uint32_t* out, size_t out_words) {
+	BN_CHECK_ARG(sc && out, "NULL argument");
+	BN_CHECK_ARG(sc->world > 1 && sc->cur <= 32, "export_shard is only valid once a shard is down to one batch");
+	BN_CHECK_ARG(out_words >= (size_t)128 * sc->d, "output needs composition_size * 128 words");
+	DeviceScope ds(sc->device);
+	for (int j = 0; j < sc->d; j++)
+		BN_HIP(hipMemcpyAsync(out + 128 * (size_t)j, sc->cols + (size_t)j * sc->col_words, 128 * sizeof(uint32_t),
+							  hipMemcpyDeviceToHost, sc->stream));
+	BN_HIP(hipStreamSynchronize(sc->stream));
+	return BN_OK;
+}
+
+extern "C" int bn_sumcheck_import_gathered(bn_sumcheck* sc, const uint32_t* words, size_t n_words, int world) {
+	BN_CHECK_ARG(sc && words, "NULL argument");
+	BN_CHECK_ARG(world == sc->world && sc->world > 1 && sc->cur <= 32, "import_gathered needs the exported state of every rank");
+	BN_CHECK_ARG(n_words >= (size_t)world * 128 * sc->d, "need world * composition_size * 128 words");
+	DeviceScope ds(sc->device);
+	// rank r's batch becomes global batch r (r < world, so batch r is owned by rank r)
+	const size_t col_words = 128 * (size_t)world;
+	std::vector<uint32_t> host((size_t)sc->d * col_words);
+	for (int r = 0; r < world; r++)
+		for (int j = 0; j < sc->d; j++)
+			memcpy(&host[(size_t)j * col_words + 128 * (size_t)r], words + ((size_t)r * sc->d + j) * 128, 128 * sizeof(uint32_t));
+	uint32_t* cols = nullptr;
+	BN_HIP(hipMalloc(&cols, sizeof(uint32_t) * host.size()));
+	hipError_t e = hipMemcpyAsync(cols, host.data(), sizeof(uint32_t) * host.size(), hipMemcpyHostToDevice, sc->stream);
+	if (e == hipSuccess) e = hipStreamSynchronize(sc->stream);
+	if (e != hipSuccess) {
+		hipFree(cols);
+		BN_FAIL(BN_ERR_HIP, "uploading gathered state: %s", hipGetErrorString(e));
+	}
+	BN_HIP(hipFree(sc->cols));
+	sc->cols = cols;
+	sc->col_words = col_words;
+	sc->cur = (size_t)32 * world;
+	sc->rank = 0;
+	sc->world = 1;
+	return BN_OK;
+}
+
+extern "C" int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32_t* points) {
+	BN_CHECK_ARG(sc && sum && points, "NULL argument");
+	BN_CHECK_ARG(!(sc->world > 1 && sc->cur <= 32), "shard exhausted: gather (export_shard/import_gathered) first");
+	DeviceScope ds(sc->device);
+	int rc = sc_launch(sc, false, nullptr);
+	if (rc != BN_OK) return rc;
+	uint32_t acc[4 * (kMaxD + 1)];
+	BN_HIP(hipMemcpyAsync(acc, sc->acc, sizeof(acc), hipMemcpyDeviceToHost, sc->stream));
+	BN_HIP(hipStreamSynchronize(sc->stream));
+	const int npts = sc->d + 1;
+	if (sc->cur == 1) {
+		memcpy(sum, acc, 16);  // mode 2 computed prod_j f_j(0) as "point 0"
+		memset(points, 0, sizeof(uint32_t) * 4 * npts);
+	} else {
+		memcpy(points, acc, sizeof(uint32_t) * 4 * npts);
+		for (int i = 0; i < 4; i++) sum[i] = acc[i] ^ acc[4 + i];
+	}
+	sc->sharded_used = true;
+	return BN_OK;
+}
+
+extern "C" int bn_sumcheck_move_to_next_round(bn_sumcheck* sc, const uint32_t* challenge) {
+	BN_CHECK_ARG(sc && challenge, "NULL argument");
+	BN_CHECK_ARG(sc->cur >= 2, "no variables left to fold");
+	BN_CHECK_ARG(!(sc->world > 1 && sc->cur <= 32), "shard exhausted: gather (export_shard/import_gathered) first");
+	DeviceScope ds(sc->device);
+	int rc = sc_launch(sc, true, challenge);
+	if (rc != BN_OK) return rc;
+	BN_HIP(hipStreamSynchronize(sc->stream));
+	sc->cur /= 2;
+	sc->round++;
+	sc->sharded_used = true;
+	return BN_OK;
+}
+
+extern "C" int bn_sumcheck_round(const bn_sumcheck* sc, int* round) {
+	BN_CHECK_ARG(sc && round, "NULL argument");
+	*round = sc->round;
+	return BN_OK;
+}
+
+extern "C" int bn_sumcheck_destroy(bn_sumcheck* sc) {
+	if (!sc) return BN_OK;
+	DeviceScope ds(sc->device);
+	sc_free(sc);
 	return BN_OK;
 }

@@ -68,6 +68,9 @@ def lib():
         "bn_sumcheck_move_to_next_round": (i32, [vp, u32p]),
         "bn_sumcheck_round": (i32, [vp, ctypes.POINTER(i32)]),
         "bn_sumcheck_set_shard": (i32, [vp, i32, i32]),
+        "bn_sumcheck_needs_gather": (i32, [vp, ctypes.POINTER(i32)]),
+        "bn_sumcheck_export_shard": (i32, [vp, u32p, sz]),
+        "bn_sumcheck_import_gathered": (i32, [vp, u32p, sz, i32]),
         "bn_sumcheck_destroy": (i32, [vp]),
     }
     for name, (res, args) in sig.items():
@@ -278,6 +281,27 @@ class Sumcheck:
     def move_to_next_round(self, challenge):
         c = np.ascontiguousarray(challenge, dtype=np.uint32).reshape(4)
         _check(lib().bn_sumcheck_move_to_next_round(self._sc, c.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))))
+
+    def round(self):
+        r = ctypes.c_int()
+        _check(lib().bn_sumcheck_round(self._sc, ctypes.byref(r)))
+        return r.value
+
+    # sharded endgame (see bn_sumcheck_needs_gather); driven by binius_ntt_amd.distributed
+    def needs_gather(self):
+        f = ctypes.c_int()
+        _check(lib().bn_sumcheck_needs_gather(self._sc, ctypes.byref(f)))
+        return bool(f.value)
+
+    def export_shard(self):
+        out = np.zeros(128 * self.d, np.uint32)
+        _check(lib().bn_sumcheck_export_shard(self._sc, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), out.size))
+        return out
+
+    def import_gathered(self, words, world):
+        w = np.ascontiguousarray(words, dtype=np.uint32).reshape(-1)
+        _check(lib().bn_sumcheck_import_gathered(self._sc, w.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), w.size,
+                                                 world))
 
     def close(self):
         if getattr(self, "_sc", None) is not None and self._sc.value:

@@ -135,6 +135,14 @@ int bn_sumcheck_round(const bn_sumcheck* sc, int* round);
  * the caller (the Python/RCCL layer does allgather + XOR). world must be a power of two
  * with 32*world <= 2^num_vars. Must be called before the first round. */
 int bn_sumcheck_set_shard(bn_sumcheck* sc, int rank, int world);
+/* Sharded endgame (no reference counterpart; the reference's analogue is the hand-over to the
+ * CPU at 32 evaluations, sumcheck.cuh:283-297): once every shard is down to one 32-element
+ * batch (*flag = 1), folds pair elements of different ranks. Each rank exports its batch
+ * (composition_size * 128 words), the caller all-gathers them rank-major and every rank
+ * imports the concatenation; the prover then continues unsharded. */
+int bn_sumcheck_needs_gather(const bn_sumcheck* sc, int* flag);
+int bn_sumcheck_export_shard(const bn_sumcheck* sc, uint32_t* out, size_t out_words);
+int bn_sumcheck_import_gathered(bn_sumcheck* sc, const uint32_t* words, size_t n_words, int world);
 int bn_sumcheck_destroy(bn_sumcheck* sc);
 
 #ifdef __cplusplus
