@@ -1,0 +1,50 @@
+// Sumcheck<NUM_VARS, COMPOSITION_SIZE, DATA_IS_TRANSPOSED> (src/ulvt/sumcheck/sumcheck.cuh:10-301)
+// over the C-ABI. Same constructor and the same two protocol methods; the evaluations are
+// COMPOSITION_SIZE columns of 4 * 2^NUM_VARS words, compact (little-endian limbs) or bitsliced
+// 128-word batches when DATA_IS_TRANSPOSED (README.md:38-45 of the reference).
+#pragma once
+
+#include <array>
+#include <chrono>
+#include <cstdint>
+#include <vector>
+
+#include "../utils/common.hpp"
+
+template <uint32_t NUM_VARS, uint32_t COMPOSITION_SIZE, bool DATA_IS_TRANSPOSED>
+class Sumcheck {
+	static constexpr uint32_t INTS_PER_VALUE = 4;
+	static constexpr uint32_t INTERPOLATION_POINTS = COMPOSITION_SIZE + 1;
+
+public:
+	// timestamps kept for source compatibility with the reference's benchmark driver
+	std::chrono::time_point<std::chrono::high_resolution_clock> start_before_memcpy;
+	std::chrono::time_point<std::chrono::high_resolution_clock> start_before_transpose;
+	std::chrono::time_point<std::chrono::high_resolution_clock> start_raw;
+
+	Sumcheck(const std::vector<uint32_t>& evals, bool benchmarking, int device = 0) {
+		if (evals.size() < (size_t)INTS_PER_VALUE * ((size_t)1 << NUM_VARS) * COMPOSITION_SIZE)
+			throw ulvt::BnError(BN_ERR_INVALID, "Sumcheck: evals shorter than COMPOSITION_SIZE * 4 * 2^NUM_VARS words");
+		if (benchmarking) start_before_memcpy = std::chrono::high_resolution_clock::now();
+		ulvt::bn_check(bn_sumcheck_create(device, NUM_VARS, COMPOSITION_SIZE, DATA_IS_TRANSPOSED ? 1 : 0, evals.data(), &sc));
+		if (benchmarking) start_before_transpose = start_raw = std::chrono::high_resolution_clock::now();
+	}
+	Sumcheck(const Sumcheck&) = delete;
+	Sumcheck& operator=(const Sumcheck&) = delete;
+	~Sumcheck() { bn_sumcheck_destroy(sc); }
+
+	void this_round_messages(std::array<uint32_t, INTS_PER_VALUE>& sum,
+							 std::array<uint32_t, INTERPOLATION_POINTS * INTS_PER_VALUE>& points) {
+		ulvt::bn_check(bn_sumcheck_round_messages(sc, sum.data(), points.data()));
+	}
+
+	void move_to_next_round(const std::array<uint32_t, INTS_PER_VALUE>& challenge) {
+		ulvt::bn_check(bn_sumcheck_move_to_next_round(sc, challenge.data()));
+	}
+
+	// multi-GPU sharding (this build's extension; see binius_ntt_amd.h)
+	void set_shard(int rank, int world) { ulvt::bn_check(bn_sumcheck_set_shard(sc, rank, world)); }
+
+private:
+	bn_sumcheck* sc = nullptr;
+};

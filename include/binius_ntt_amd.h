@@ -96,7 +96,8 @@ int bn_gf32_mul_device(const void* d_a, const void* d_b, void* d_out, size_t n, 
  * (src/ulvt/finite_fields/tests/profiling/kernels/bitsliced_repeat.cu:5-32):
  * kind 0 = compact GF(2^128), kind 1 = bitsliced GF(2^128) (32 products per lane-block).
  * Each of `threads` lanes performs `iters` dependent products; d_state holds
- * threads*4 (kind 0) or threads*128 (kind 1) words, updated in place. */
+ * threads*4 (kind 0) or threads*128 (kind 1) words, updated in place, and d_operand holds
+ * the lanes' multipliers in the same shape (threads*4 or threads*128 words). */
 int bn_gf128_mul_repeat_device(int kind, void* d_state, const void* d_operand, size_t threads, int iters, void* stream);
 
 /* ------------------------------------------------------------------------------------
@@ -114,7 +115,8 @@ typedef struct bn_sumcheck bn_sumcheck;
 /* Replaces Sumcheck<NUM_VARS, COMPOSITION_SIZE, DATA_IS_TRANSPOSED>(evals, benchmarking)
  * (sumcheck.cuh:82-126). evals: composition_size columns of 4*2^num_vars words each,
  * column-major; compact when data_is_transposed == 0 (converted on the device), bitsliced
- * 128-word blocks otherwise. 1 <= num_vars <= 30, 1 <= composition_size <= 8.
+ * 128-word blocks otherwise. 1 <= num_vars <= 30 (>= 5 for bitsliced input),
+ * 1 <= composition_size <= 8.
  * The host copy is made synchronously. */
 int bn_sumcheck_create(int device, int num_vars, int composition_size, int data_is_transposed,
                        const uint32_t* evals, bn_sumcheck** sc);

@@ -1,0 +1,132 @@
+#!/usr/bin/env python3
+"""Secondary benchmark lines for BASELINE.json configs 2-5 (bench.py keeps the headline NTT).
+
+  python tools/bench_configs.py [--only c2,c3,c4,c5] [--sc-vars 24] [--out FILE]
+
+c2  GF(2^128) multiply microbench, register-resident repeat loops (bitsliced_repeat style):
+    compact (one element per lane) and bitsliced (32 products per lane-block), products/s.
+c3  2^20-point GF(2^128) additive NTT, device-resident, elements/s.
+c4  Sumcheck over GF(2^128), 2^N evals, bitsliced input (DATA_IS_TRANSPOSED = true),
+    d in {2,3,4}: all N rounds (messages + fold) plus the final messages, device-resident
+    columns; evals/s = 2^N / t.  Synthetic evals (numpy PCG64, fixed seed) and challenges.
+c5  one GPU's share of the 256 x 2^20 batched NTT (32 transforms), elements/s.
+Every line is one JSON object.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "binius-ntt_amd", "python"))
+
+import numpy as np  # noqa: E402
+
+
+def ev_time(fn, reps, stream):
+    import torch
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    a.record(stream)
+    for _ in range(reps):
+        fn()
+    b.record(stream)
+    b.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def c2(dev, out):
+    import torch
+    import binius_ntt_amd as B
+    st = torch.cuda.current_stream(dev)
+    g = np.random.default_rng(2)
+    for kind, name, words, per in ((0, "compact", 4, 1), (1, "bitsliced", 128, 32)):
+        threads = 256 * 2048 if kind == 0 else 256 * 1024
+        iters = 2000 if kind == 0 else 20
+        state = torch.from_numpy(g.integers(0, 2**32, size=threads * words, dtype=np.uint64).astype(np.uint32)
+                                 .view(np.int32)).to(dev)
+        opnd = torch.from_numpy(g.integers(0, 2**32, size=threads * words, dtype=np.uint64).astype(np.uint32)
+                                .view(np.int32)).to(dev)  # one multiplier per lane, same shape as state
+        ms = ev_time(lambda: B.gf128_mul_repeat(kind, state, opnd, threads, iters, stream=st), 3, st)
+        prods = threads * iters * per
+        out({"config": "c2", "workload": "GF(2^128) multiply repeat loop, %s" % name, "value": prods / (ms * 1e-3),
+             "unit": "products/s", "ms": ms, "threads": threads, "iters": iters})
+
+
+def ntt_line(dev, out, cfg, log_h, batch):
+    import torch
+    import binius_ntt_amd as B
+    n = 1 << log_h
+    g = np.random.default_rng(3)
+    x = torch.from_numpy(g.integers(0, 2**32, size=4 * n * batch, dtype=np.uint64).astype(np.uint32)
+                         .view(np.int32)).to(dev)
+    y = torch.empty_like(x)
+    ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(7), device=dev.index or 0))
+    st = torch.cuda.current_stream(dev)
+    ms = ev_time(lambda: ntt.forward_device(x, y, batch=batch, stream=st), 10, st)
+    elems = n * batch
+    out({"config": cfg, "workload": "%d x 2^%d-point GF(2^128) additive NTT (r=0)" % (batch, log_h),
+         "value": elems / (ms * 1e-3), "unit": "elements/s", "ms": ms,
+         "hbm_gbps_algorithmic": 32.0 * elems / (ms * 1e-3) / 1e9})
+
+
+def c4(dev, out, nvars, ds):
+    import torch
+    import binius_ntt_amd as B
+    for d in ds:
+        g = np.random.default_rng(0x5C00 + d)
+        words = 4 * (1 << nvars) * d
+        ev = torch.from_numpy(g.integers(0, 2**32, size=words, dtype=np.uint64).astype(np.uint32)
+                              .view(np.int32)).to(dev)
+        ch = g.integers(0, 2**32, size=(nvars, 4), dtype=np.uint64).astype(np.uint32)
+        torch.cuda.synchronize()
+        sc = B.Sumcheck(nvars, d, True, ev)  # copies the columns (device to device)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for r in range(nvars):
+            sc.this_round_messages()
+            sc.move_to_next_round(ch[r])
+        sc.this_round_messages()
+        dt = time.perf_counter() - t0
+        sc.close()
+        del ev
+        torch.cuda.empty_cache()
+        out({"config": "c4", "workload": "sumcheck GF(2^128), 2^%d evals, d=%d, bitsliced input" % (nvars, d),
+             "value": (1 << nvars) / dt, "unit": "evals/s", "ms": dt * 1e3,
+             "hbm_gbps_algorithmic": 3.0 * d * 16 * (1 << nvars) / dt / 1e9})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="c2,c3,c4,c5")
+    ap.add_argument("--sc-vars", type=int, default=24)
+    ap.add_argument("--sc-d", default="2,3,4")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    import torch
+    dev = torch.device("cuda", 0)
+    lines = []
+
+    def out(d):
+        lines.append(d)
+        print(json.dumps(d), flush=True)
+
+    only = set(a.only.split(","))
+    if "c2" in only:
+        c2(dev, out)
+    if "c3" in only:
+        ntt_line(dev, out, "c3", 20, 1)
+    if "c4" in only:
+        c4(dev, out, a.sc_vars, [int(x) for x in a.sc_d.split(",")])
+    if "c5" in only:
+        ntt_line(dev, out, "c5 (per-GPU share)", 20, 32)
+    if a.out:
+        with open(a.out, "w") as f:
+            for d in lines:
+                f.write(json.dumps(d) + "\n")
+
+
+if __name__ == "__main__":
+    main()
