@@ -3,35 +3,65 @@
 
 Per MI355X_MICROARCH.md (HBM section): FETCH_SIZE reports half the bytes of wide coalesced
 streaming reads on gfx950 -> doubled here; WRITE_SIZE reads exact for 16-B stores. Both are
-in KiB. Prints per-kernel mean per dispatch.
+in KiB. Prints the per-kernel mean per dispatch and writes gpurun_out/pmc_summary.json.
+With --traffic LOG_H it also writes profiles/pmc_traffic.json: {LOG_H: HBM bytes per launch of
+the headline NTT's dominant kernel (the bottom pass, antt_bs_pass<4, 2>)}, read by bench.py.
 """
-import csv, glob, json, os, sys
+import csv
+import glob
+import json
+import os
+import sys
 from collections import defaultdict
-root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-acc = defaultdict(lambda: defaultdict(list))
-for f in glob.glob(os.path.join(root, "pmc_*", "run_counter_collection.csv")):
-    per = defaultdict(lambda: defaultdict(float))
-    meta = {}
-    for row in csv.DictReader(open(f)):
-        key = (row["Dispatch_Id"], row["Kernel_Name"])
-        per[key][row["Counter_Name"]] += float(row["Counter_Value"])
-        meta[key] = row
-    for (d, k), cs in per.items():
-        for c, v in cs.items():
-            acc[k][c].append(v)
-out = {}
-for k, cs in acc.items():
-    if "rocclr" in k:
-        continue
-    m = {c: sum(v) / len(v) for c, v in cs.items()}
-    if "FETCH_SIZE" in m:
-        m["HBM_READ_BYTES_corrected"] = 2 * m["FETCH_SIZE"] * 1024
-    if "WRITE_SIZE" in m:
-        m["HBM_WRITE_BYTES"] = m["WRITE_SIZE"] * 1024
-    if "SQ_ACTIVE_INST_VALU" in m and "SQ_BUSY_CYCLES" in m:
-        pass
-    out[k] = m
-    print(k)
-    for c in sorted(m):
-        print("   %-28s %.4g" % (c, m[c]))
-json.dump(out, open(os.path.join(root, "pmc_summary.json"), "w"), indent=1)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    args = sys.argv[1:]
+    traffic_log_h = None
+    if "--traffic" in args:
+        i = args.index("--traffic")
+        traffic_log_h = args[i + 1]
+        del args[i:i + 2]
+    root = args[0] if args else os.path.join(ROOT, "gpurun_out")
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(root, "pmc_*", "run_counter_collection.csv")):
+        per = defaultdict(lambda: defaultdict(float))
+        for row in csv.DictReader(open(f)):
+            per[(row["Dispatch_Id"], row["Kernel_Name"])][row["Counter_Name"]] += float(row["Counter_Value"])
+        for (_, k), cs in per.items():
+            for c, v in cs.items():
+                acc[k][c].append(v)
+    out = {}
+    for k, cs in acc.items():
+        if "rocclr" in k:
+            continue
+        m = {c: sum(v) / len(v) for c, v in cs.items()}
+        if "FETCH_SIZE" in m:
+            m["HBM_READ_BYTES_corrected"] = 2 * m["FETCH_SIZE"] * 1024
+        if "WRITE_SIZE" in m:
+            m["HBM_WRITE_BYTES"] = m["WRITE_SIZE"] * 1024
+        out[k] = m
+        print(k)
+        for c in sorted(m):
+            print("   %-28s %.4g" % (c, m[c]))
+    with open(os.path.join(root, "pmc_summary.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    if traffic_log_h:
+        dom = [k for k in out if "antt_bs_pass<4, 2>" in k]
+        if dom and "HBM_READ_BYTES_corrected" in out[dom[0]] and "HBM_WRITE_BYTES" in out[dom[0]]:
+            m = out[dom[0]]
+            path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            cur = json.load(open(path)) if os.path.exists(path) else {}
+            cur[traffic_log_h] = m["HBM_READ_BYTES_corrected"] + m["HBM_WRITE_BYTES"]
+            cur["_kernel_" + traffic_log_h] = dom[0]
+            cur["_read_bytes_" + traffic_log_h] = m["HBM_READ_BYTES_corrected"]
+            cur["_write_bytes_" + traffic_log_h] = m["HBM_WRITE_BYTES"]
+            with open(path, "w") as f:
+                json.dump(cur, f, indent=1)
+            print("traffic per launch of %s: %.4g B" % (dom[0], cur[traffic_log_h]))
+
+
+if __name__ == "__main__":
+    main()
