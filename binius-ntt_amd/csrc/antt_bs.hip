@@ -62,7 +62,8 @@ struct BsParams {
 	const uint32_t* src;
 	uint32_t* dst;
 	int log_h, log_rate;
-	int dbg;  // timing experiments only (BN_DEBUG_FLAGS): 1 no loads, 2 no stores, 4 no multiplies
+	int dbg;  // timing experiments only (BN_DEBUG_FLAGS): 1 no loads, 2 no stores, 4 no multiplies,
+	          // 8 no stage barriers, 16 no in-word stages, 32 no tile-bit stages
 	BsPass p;
 };
 
@@ -223,8 +224,8 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 	};
 	const int jlow = max(LAST ? 5 : 0, ps.stop_j);
 	for (int j = ps.k - 1; j >= jlow; j--) {
-		block_stage(j, tid / L);
-		__syncthreads();
+		if (!(P.dbg & 32)) block_stage(j, tid / L);
+		if (!(P.dbg & 8)) __syncthreads();
 	}
 
 	if (LAST) {
@@ -235,7 +236,7 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 		const int qa = tid / L, qb = qa | (kTileBlocks / 2);
 		uint32_t* pa = lds + qa * BLK_WORDS + l * kLimbStride;
 		uint32_t* pb = lds + qb * BLK_WORDS + l * kLimbStride;
-		for (int s = 4; s >= ps.stop_j; s--) {  // the bottom pass starts at stage 0: j == s
+		for (int s = 4; s >= ((P.dbg & 16) ? 5 : ps.stop_j); s--) {  // bottom pass starts at stage 0: j == s
 			{
 				const int d = 1 << s;
 				const uint32_t um = ~lane_mask(s);

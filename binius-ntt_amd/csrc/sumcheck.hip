@@ -36,16 +36,15 @@ namespace {
 
 constexpr int kScThreads = 256;
 constexpr int kQuadsPerWG = kScThreads / 4;
-constexpr int kQuadWords = 256;  // LDS words per quad
+constexpr int kRowWords = 36;    // LDS words per 32-word row (padding: bank spread)
+constexpr int kQuadWords = 304;  // LDS words per quad slot (8 padded rows + spread)
 constexpr int kMaxD = 8;
 
 // compiler ordering for LDS traffic between lanes of one wave (the hardware executes a wave's
 // LDS instructions in order)
 __device__ __forceinline__ void wsync() {
 	asm volatile("" ::: "memory");
-	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 	__builtin_amdgcn_wave_barrier();
-	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __device__ __forceinline__ void ld32(uint32_t* r, const uint32_t* p) {
@@ -74,72 +73,96 @@ __device__ __forceinline__ void bs_alpha(const uint32_t* a, uint32_t* out) {
 	}
 }
 
-// GF(2^128) product inside a quad's LDS slot S (256 words). On entry S[32l..32l+32) holds limb
-// l of the first operand and B[32l..32l+32) limb l of the second (B = S + 128, or a shared
-// broadcast operand elsewhere in LDS). On exit S[32l..32l+32) holds limb l of the product.
-__device__ __forceinline__ void quad_mul(uint32_t* S, const uint32_t* B, int l) {
+// A quad's LDS slot: 8 rows of 32 words, rows padded to 36 words and slots to 304 words. With
+// that padding the access patterns of quad_mul (operand rows l and 4+l, product rows 2l and
+// 2l+1, the cross-lane reads) are nearly free of bank conflicts for both the 16-lane
+// ds_read_b128 groups and the 8-lane ds_write_b128 groups (3328 -> 192 extra cycles per product
+// in a lane-group model), while every address stays a base plus an immediate offset.
+struct Slot {
+	uint32_t* base;
+	__device__ __forceinline__ uint32_t* row(int r) const { return base + kRowWords * r; }
+};
+__device__ __forceinline__ void sld(uint32_t* x, const Slot& S, int r) { ld32(x, S.row(r)); }
+__device__ __forceinline__ void sst(const Slot& S, int r, const uint32_t* x) { st32(S.row(r), x); }
+
+// GF(2^128) product on a quad. On entry slot row l holds limb l of the first operand and row 4+l
+// limb l of the second — or, with B_SHARED, the second operand is the unswizzled 128-word B
+// shared by every quad (the fold's broadcast challenge). On exit row l holds limb l of the product.
+template <bool B_SHARED>
+__device__ __forceinline__ void quad_mul(const Slot& S, const uint32_t* B, int l) {
 	wsync();
 	const int ia = l & 1, jb = (l == 1 || l == 2) ? 1 : 0;
-	const uint32_t* A0 = S + 64 * ia;
-	const uint32_t* B0 = B + 64 * jb;
+	const int ra = 2 * ia, rb = 4 + 2 * jb;  // rows of a0 (a1 = ra + 1) and b0 (b1 = rb + 1)
+	auto ldb = [&](uint32_t* x, int h) {
+		if constexpr (B_SHARED)
+			ld32(x, B + 64 * jb + 32 * h);
+		else
+			sld(x, S, rb + h);
+	};
 	uint32_t x[32], y[32], z[32];
 	// GF(2^64) Karatsuba: z0 = a0 b0, z2 = a1 b1, z1 = (a0+a1)(b0+b1) + z0 + z2; at most one
 	// 32-word value is live across a circuit (the circuits themselves need ~160 VGPRs), the
 	// rest is parked in the quad's LDS slot once the operands have been consumed.
-	ld32(x, A0);
-	ld32(y, B0);
+	sld(x, S, ra);
+	ldb(y, 0);
 	bsm5_mul(x, y, z);  // z0
 	__builtin_amdgcn_sched_barrier(0);
-	ld32(x, A0 + 32);
-	ld32(y, B0 + 32);
+	wsync();  // also a compiler memory barrier: operands are re-read, never kept live
+	sld(x, S, ra + 1);
+	ldb(y, 1);
 	bsm5_mul(x, y, y);  // z2
 	__builtin_amdgcn_sched_barrier(0);
+	wsync();
 #pragma unroll
 	for (int i = 0; i < 32; i++) z[i] ^= y[i];  // lo = z0 + z2
 	bs_alpha<5>(y, x);
 #pragma unroll
 	for (int i = 0; i < 32; i++) y[i] = z[i] ^ x[i];  // lo + alpha(z2)
 	uint32_t sa[32], sb[32];
+	{
+		const uint32_t* A0 = S.row(ra);
+		const uint32_t* B0 = B_SHARED ? B + 64 * jb : S.row(rb);
+		const int bstep = B_SHARED ? 32 : kRowWords;
 #pragma unroll
-	for (int i = 0; i < 32; i += 4) {
-		const uint4 p = *(const uint4*)(A0 + i), q = *(const uint4*)(A0 + 32 + i);
-		const uint4 u = *(const uint4*)(B0 + i), v = *(const uint4*)(B0 + 32 + i);
-		sa[i] = p.x ^ q.x, sa[i + 1] = p.y ^ q.y, sa[i + 2] = p.z ^ q.z, sa[i + 3] = p.w ^ q.w;
-		sb[i] = u.x ^ v.x, sb[i + 1] = u.y ^ v.y, sb[i + 2] = u.z ^ v.z, sb[i + 3] = u.w ^ v.w;
+		for (int i = 0; i < 32; i += 4) {
+			const uint4 p = *(const uint4*)(A0 + i), q = *(const uint4*)(A0 + kRowWords + i);
+			const uint4 u = *(const uint4*)(B0 + i), v = *(const uint4*)(B0 + bstep + i);
+			sa[i] = p.x ^ q.x, sa[i + 1] = p.y ^ q.y, sa[i + 2] = p.z ^ q.z, sa[i + 3] = p.w ^ q.w;
+			sb[i] = u.x ^ v.x, sb[i + 1] = u.y ^ v.y, sb[i + 2] = u.z ^ v.z, sb[i + 3] = u.w ^ v.w;
+		}
 	}
 	wsync();  // every lane of the quad has read its operands: the slot is free
-	st32(S + 64 * l, z);
-	st32(S + 64 * l + 32, y);
+	sst(S, 2 * l, z);
+	sst(S, 2 * l + 1, y);
 	__builtin_amdgcn_sched_barrier(0);
 	bsm5_mul(sa, sb, x);  // (a0+a1)(b0+b1)
 	__builtin_amdgcn_sched_barrier(0);
-	ld32(y, S + 64 * l + 32);
+	sld(y, S, 2 * l + 1);
 #pragma unroll
 	for (int i = 0; i < 32; i++) x[i] ^= y[i];  // hi = z1 + alpha(z2)
-	st32(S + 64 * l + 32, x);
+	sst(S, 2 * l + 1, x);
 	wsync();
-	// lane l assembles limb l: limbs 0,1 = P00 + P11; limbs 2,3 = P01 + P10 + alpha64(P11),
-	// alpha64(P) = (P.hi, P.lo + alpha(P.hi))
-	const int p0 = l < 2 ? 0 : 2, half = l & 1;
+	// lane q's GF(2^64) product P_q = (lo, hi) sits in rows 2q, 2q+1. Lane l assembles limb l:
+	// limbs 0,1 = P00 + P11; limbs 2,3 = P01 + P10 + alpha64(P11), alpha64(P) = (P.hi, P.lo + alpha(P.hi))
+	const int e0 = 2 * (l < 2 ? 0 : 2) + (l & 1);
 	const uint32_t m2 = (l == 2) ? ~0u : 0u, m3 = (l == 3) ? ~0u : 0u;
-	ld32(x, S + 64 * 1 + 32);  // P11.hi
-	bs_alpha<5>(x, y);
+	sld(z, S, e0);
+	sld(x, S, e0 + 2);
 #pragma unroll
-	for (int i = 0; i < 32; i++) {
-		const uint32_t e = S[64 * p0 + 32 * half + i] ^ S[64 * (p0 + 1) + 32 * half + i];
-		z[i] = e ^ (x[i] & m2) ^ ((S[64 + i] ^ y[i]) & m3);
-	}
+	for (int i = 0; i < 32; i++) z[i] ^= x[i];
+	sld(x, S, 3);  // P11.hi
+	bs_alpha<5>(x, y);
+	sld(sa, S, 2);  // P11.lo
+#pragma unroll
+	for (int i = 0; i < 32; i++) z[i] ^= (x[i] & m2) ^ ((sa[i] ^ y[i]) & m3);
 	wsync();
-	st32(S + 32 * l, z);
+	sst(S, l, z);
 	wsync();
 }
 
-// out = k * x for a tower constant k < 16 acting on the 8 GF(2^4) coordinates of a limb
-// (alias-safe)
-__device__ __forceinline__ void mul_small(uint32_t k, const uint32_t* x, uint32_t* out) {
-	uint32_t c[4];
-#pragma unroll
-	for (int a = 0; a < 4; a++) c[a] = (uint32_t)tw_mul(k, 1u << a, 2);
+// out = k * x for a tower constant k < 16 acting on the 8 GF(2^4) coordinates of a limb; c[a]
+// is the GF(2^4) product k * 2^a (host-computed, ScArgs::kcol). Alias-safe.
+__device__ __forceinline__ void mul_small(const uint32_t* c, const uint32_t* x, uint32_t* out) {
 #pragma unroll
 	for (int g = 0; g < 8; g++) {
 		uint32_t r[4];
@@ -173,6 +196,7 @@ struct ScArgs {
 	int kmax;           // points 0..kmax
 	uint32_t r[4];      // fold challenge
 	uint32_t* acc;      // (kmax + 1) x 4 words, XOR-accumulated
+	uint32_t kcol[kMaxD + 1][4];  // GF(2^4) products k * 2^a (interpolation point k)
 };
 
 // lo/hi limbs of column j for pair p (this lane's limb l)
@@ -208,11 +232,13 @@ template <int MODE>
 __global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
 	extern __shared__ uint32_t lds[];
 	const int l = threadIdx.x & 3, qw = threadIdx.x >> 2;
-	uint32_t* S = lds + qw * kQuadWords;
-	const size_t quad0 = (size_t)blockIdx.x * kQuadsPerWG + qw, nquads = (size_t)gridDim.x * kQuadsPerWG;
-	for (int k = 0; k <= A.kmax; k++) {
+	const Slot S{lds + qw * kQuadWords};
+	const size_t quad0 = (size_t)blockIdx.x * kQuadsPerWG + qw;
+	{  // one interpolation point per grid row
+		const int k = blockIdx.y;
 		uint32_t acc = 0;
-		for (size_t p = quad0; p < A.n_pairs; p += nquads) {
+		const size_t p = quad0;
+		if (p < A.n_pairs) {  // one pair per quad (no grid-stride loop: it costs registers)
 			uint32_t emask = 0;
 			for (int j = 0; j < A.d; j++) {
 				// f_j at point k: lo + k (lo + hi), written into the A (j == 0) or B operand
@@ -225,16 +251,16 @@ __global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
 				} else {
 #pragma unroll
 					for (int i = 0; i < 32; i++) hi[i] ^= lo[i];
-					mul_small((uint32_t)k, hi, hi);
+					mul_small(A.kcol[k], hi, hi);
 #pragma unroll
 					for (int i = 0; i < 32; i++) lo[i] ^= hi[i];
 				}
-				st32(S + (j == 0 ? 0 : 128) + 32 * l, lo);
-				if (j > 0) quad_mul(S, S + 128, l);
+				sst(S, (j == 0 ? 0 : 4) + l, lo);
+				if (j > 0) quad_mul<false>(S, nullptr, l);
 			}
 			wsync();
 			uint32_t t[32];
-			ld32(t, S + 32 * l);
+			sld(t, S, l);
 			acc ^= parity_word(t, emask);
 			wsync();
 		}
@@ -251,24 +277,25 @@ template <int MODE>
 __global__ __launch_bounds__(kScThreads, 2) void sc_fold(ScArgs A) {
 	extern __shared__ uint32_t lds[];
 	const int l = threadIdx.x & 3, qw = threadIdx.x >> 2;
-	uint32_t* S = lds + qw * kQuadWords;
+	const Slot S{lds + qw * kQuadWords};
 	uint32_t* R = lds + kQuadsPerWG * kQuadWords;  // the challenge, broadcast-bitsliced, shared
 	if (threadIdx.x < 128) R[threadIdx.x] = 0u - ((A.r[threadIdx.x / 32] >> (threadIdx.x % 32)) & 1u);
 	__syncthreads();
-	const size_t quad0 = (size_t)blockIdx.x * kQuadsPerWG + qw, nquads = (size_t)gridDim.x * kQuadsPerWG;
+	const size_t quad0 = (size_t)blockIdx.x * kQuadsPerWG + qw;
 	const size_t items = (size_t)A.d * A.n_pairs;
-	for (size_t it = quad0; it < items; it += nquads) {
+	const size_t it = quad0;
+	if (it < items) {  // one item per quad (no grid-stride loop: it costs registers)
 		const int j = (int)(it / A.n_pairs);
 		const size_t p = it % A.n_pairs;
 		uint32_t lo[32], hi[32], emask;
 		load_pair<MODE>(A, j, p, l, lo, hi, emask);
 #pragma unroll
 		for (int i = 0; i < 32; i++) hi[i] ^= lo[i];
-		st32(S + 32 * l, hi);
-		quad_mul(S, R, l);
+		sst(S, l, hi);
+		quad_mul<true>(S, R, l);
 		// lo is re-read (cache-resident) rather than kept live across the product
 		load_pair<MODE>(A, j, p, l, lo, hi, emask);
-		ld32(hi, S + 32 * l);
+		sld(hi, S, l);
 #pragma unroll
 		for (int i = 0; i < 32; i++) lo[i] = (lo[i] ^ hi[i]) & emask;
 		wsync();
@@ -303,6 +330,7 @@ struct bn_sumcheck {
 	size_t col_words = 0;   // words between columns (allocation)
 	uint32_t* cols = nullptr;
 	uint32_t* acc = nullptr;
+	uint32_t* h_acc = nullptr;  // pinned host copy of acc (round messages)
 	hipStream_t stream = nullptr;
 	bool sharded_used = false;
 };
@@ -333,14 +361,16 @@ int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 	}
 	A.acc = sc->acc;
 	if (fold) memcpy(A.r, r, 16);
+	for (int k = 0; k <= kMaxD; k++)
+		for (int a = 0; a < 4; a++) A.kcol[k][a] = (uint32_t)tw_mul((uint64_t)k, 1ull << a, 2);
 	const size_t items = fold ? (size_t)sc->d * A.n_pairs : A.n_pairs;
-	size_t grid = (items + kQuadsPerWG - 1) / kQuadsPerWG;
-	if (grid > 4096) grid = 4096;
+	const unsigned rows = fold ? 1u : (unsigned)(A.kmax + 1);  // messages: grid row = point k
+	const size_t grid = (items + kQuadsPerWG - 1) / kQuadsPerWG;  // one item per quad
 	if (!fold) BN_HIP(hipMemsetAsync(sc->acc, 0, sizeof(uint32_t) * 4 * (kMaxD + 1), sc->stream));
 	void* args[] = {&A};
 	const void* fns[2][3] = {{(const void*)sc_messages<0>, (const void*)sc_messages<1>, (const void*)sc_messages<2>},
 							 {(const void*)sc_fold<0>, (const void*)sc_fold<1>, (const void*)sc_fold<2>}};
-	BN_HIP(hipLaunchKernel(fns[fold ? 1 : 0][A.mode], dim3((unsigned)grid), dim3(kScThreads),
+	BN_HIP(hipLaunchKernel(fns[fold ? 1 : 0][A.mode], dim3((unsigned)grid, rows), dim3(kScThreads),
 						   args, lds_bytes(), sc->stream));
 	return BN_OK;
 }
@@ -354,6 +384,7 @@ int sc_alloc(bn_sumcheck* sc, size_t col_words) {
 int sc_common_init(bn_sumcheck* sc) {
 	BN_HIP(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
 	BN_HIP(hipMalloc(&sc->acc, sizeof(uint32_t) * 4 * (kMaxD + 1)));
+	BN_HIP(hipHostMalloc((void**)&sc->h_acc, sizeof(uint32_t) * 4 * (kMaxD + 1), hipHostMallocDefault));
 	const void* fns[6] = {(const void*)sc_messages<0>, (const void*)sc_messages<1>, (const void*)sc_messages<2>,
 						  (const void*)sc_fold<0>,     (const void*)sc_fold<1>,     (const void*)sc_fold<2>};
 	for (const void* f : fns) BN_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes()));
@@ -365,6 +396,7 @@ void sc_free(bn_sumcheck* sc) {
 	if (sc->stream) hipStreamSynchronize(sc->stream);
 	if (sc->cols) hipFree(sc->cols);
 	if (sc->acc) hipFree(sc->acc);
+	if (sc->h_acc) hipHostFree(sc->h_acc);
 	if (sc->stream) hipStreamDestroy(sc->stream);
 	delete sc;
 }
@@ -558,8 +590,8 @@ extern "C" int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32
 	DeviceScope ds(sc->device);
 	int rc = sc_launch(sc, false, nullptr);
 	if (rc != BN_OK) return rc;
-	uint32_t acc[4 * (kMaxD + 1)];
-	BN_HIP(hipMemcpyAsync(acc, sc->acc, sizeof(acc), hipMemcpyDeviceToHost, sc->stream));
+	const uint32_t* acc = sc->h_acc;
+	BN_HIP(hipMemcpyAsync(sc->h_acc, sc->acc, sizeof(uint32_t) * 4 * (kMaxD + 1), hipMemcpyDeviceToHost, sc->stream));
 	BN_HIP(hipStreamSynchronize(sc->stream));
 	const int npts = sc->d + 1;
 	if (sc->cur == 1) {
@@ -580,7 +612,7 @@ extern "C" int bn_sumcheck_move_to_next_round(bn_sumcheck* sc, const uint32_t* c
 	DeviceScope ds(sc->device);
 	int rc = sc_launch(sc, true, challenge);
 	if (rc != BN_OK) return rc;
-	BN_HIP(hipStreamSynchronize(sc->stream));
+	// no sync: the fold is ordered before the next round's messages on the prover's stream
 	sc->cur /= 2;
 	sc->round++;
 	sc->sharded_used = true;
