@@ -79,6 +79,8 @@ __global__ __launch_bounds__(256) void antt_v0_group(V0Params p) {
 	const uint32_t* src = p.first ? p.src : (p.dst + (size_t)coset * n * L);
 	uint32_t* dst = p.dst + (size_t)coset * n * L;
 
+	uint8_t* tab = (uint8_t*)(lds + (size_t)tile * L);  // GF(2^8) log/exp tables after the tile
+	gf8_tables_to_lds(tab);
 	for (int pos = threadIdx.x; pos < tile; pos += blockDim.x) {
 		const size_t gi = gidx(pos);
 #pragma unroll
@@ -102,7 +104,7 @@ __global__ __launch_bounds__(256) void antt_v0_group(V0Params p) {
 #pragma unroll
 			for (int l = 0; l < L; l++) {
 				uint32_t u = lds[pu * L + l], v = lds[pv * L + l];
-				u ^= dmul<5>(w, v);
+				u ^= (uint32_t)dmul_t<5>(w, v, tab);
 				v ^= u;
 				lds[pu * L + l] = u;
 				lds[pv * L + l] = v;
@@ -157,7 +159,9 @@ int launch_v0(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, hipStre
 		const int c = std::min(lo, kTileLog - k);
 		V0Params p{d_in, d_out, plan->s_dev, plan->width, log_h, plan->log_rate, lo, k, c, first ? 1 : 0};
 		const size_t blocks = ((size_t)1 << (log_h - k - c)) << plan->log_rate;
-		const size_t lds = ((size_t)1 << (k + c)) * L * sizeof(uint32_t);
+		const size_t lds = ((size_t)1 << (k + c)) * L * sizeof(uint32_t) + kGf8LdsBytes;
+		const void* fn = L == 4 ? (const void*)antt_v0_group<4> : (const void*)antt_v0_group<1>;
+		BN_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
 		int rc = timing_begin(plan, kind, st);
 		if (rc != BN_OK) return rc;
 		if (L == 4)

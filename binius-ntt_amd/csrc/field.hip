@@ -9,14 +9,21 @@
 
 namespace bn {
 
-__global__ void k_gf32_mul(const uint32_t* a, const uint32_t* b, uint32_t* o, size_t n) {
+// Compact products: Karatsuba down to GF(2^8), whose products are log/exp lookups in LDS.
+__global__ __launch_bounds__(256) void k_gf32_mul(const uint32_t* a, const uint32_t* b, uint32_t* o, size_t n) {
+	__shared__ uint8_t tab[kGf8LdsBytes];
+	gf8_tables_to_lds(tab);
+	__syncthreads();
 	for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-		o[i] = dmul<5>(a[i], b[i]);
+		o[i] = (uint32_t)dmul_t<5>(a[i], b[i], tab);
 }
 
-__global__ void k_gf128_mul(const uint4* a, const uint4* b, uint4* o, size_t n) {
+__global__ __launch_bounds__(256) void k_gf128_mul(const uint4* a, const uint4* b, uint4* o, size_t n) {
+	__shared__ uint8_t tab[kGf8LdsBytes];
+	gf8_tables_to_lds(tab);
+	__syncthreads();
 	for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-		o[i] = dmul128(a[i], b[i]);
+		o[i] = dmul128_t(a[i], b[i], tab);
 }
 
 // One thread per 128-word block (transpose_kernel / untranspose_kernel,
@@ -53,11 +60,14 @@ __global__ __launch_bounds__(256) void k_gf128_mul_bs(const uint32_t* a, const u
 // bitsliced_repeat-style microbenchmarks (src/ulvt/finite_fields/tests/profiling/kernels/
 // bitsliced_repeat.cu:5-32): `iters` dependent products per lane, operands register-resident.
 __global__ __launch_bounds__(256) void k_repeat_compact(uint4* state, const uint4* operand, size_t threads, int iters) {
+	__shared__ uint8_t tab[kGf8LdsBytes];
+	gf8_tables_to_lds(tab);
+	__syncthreads();
 	const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
 	if (t >= threads) return;
 	uint4 x = state[t];
 	const uint4 y = operand[t];
-	for (int i = 0; i < iters; i++) x = dmul128(x, y);
+	for (int i = 0; i < iters; i++) x = dmul128_t(x, y, tab);
 	state[t] = x;
 }
 

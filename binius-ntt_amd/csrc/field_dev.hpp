@@ -5,7 +5,85 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tower.hpp"
+
 namespace bn {
+
+// ---- GF(2^8) of the tower by log/exp tables (compact arithmetic leaves) ----
+struct Gf8Tables {
+	uint8_t lg[256];
+	uint8_t ex[512];  // ex[i] = g^i for i < 510 (no modular reduction needed for lg[a] + lg[b])
+};
+constexpr Gf8Tables make_gf8_tables() {
+	Gf8Tables t{};
+	uint64_t g = 2;
+	for (;; g++) {  // smallest generator of the tower GF(2^8)^*
+		uint64_t x = g;
+		int order = 1;
+		while (x != 1) {
+			x = tw_mul(x, g, 3);
+			order++;
+		}
+		if (order == 255) break;
+	}
+	uint64_t x = 1;
+	for (int i = 0; i < 512; i++) {
+		t.ex[i] = (uint8_t)x;
+		if (i < 255) t.lg[x] = (uint8_t)i;
+		x = tw_mul(x, g, 3);
+	}
+	return t;
+}
+__constant__ constexpr Gf8Tables kGf8 = make_gf8_tables();
+constexpr int kGf8LdsBytes = 768;
+
+// Copy the tables into (at least 768 bytes of) LDS; the caller synchronises.
+__device__ __forceinline__ void gf8_tables_to_lds(uint8_t* lds_tab) {
+	const uint32_t* src = (const uint32_t*)&kGf8;
+	for (int i = threadIdx.x; i < kGf8LdsBytes / 4; i += blockDim.x) ((uint32_t*)lds_tab)[i] = src[i];
+}
+
+__device__ __forceinline__ uint32_t gf8_mul(uint32_t a, uint32_t b, const uint8_t* tab) {
+	const uint32_t r = tab[256 + tab[a] + tab[b]];
+	return (a && b) ? r : 0u;
+}
+
+// multiply_alpha on the low 2^H bits of a u64 (compile-time height, no recursion at run time)
+template <int H>
+__device__ __forceinline__ uint64_t dmul_alpha_u64(uint64_t a) {
+	if constexpr (H == 0) {
+		return a & 1u;
+	} else {
+		constexpr int half = 1 << (H - 1);
+		constexpr uint64_t m = (half >= 64) ? ~0ull : ((1ull << half) - 1ull);
+		const uint64_t a0 = a & m, a1 = (a >> half) & m;
+		return a1 | ((a0 ^ dmul_alpha_u64<H - 1>(a1)) << half);
+	}
+}
+
+// Compact Karatsuba with GF(2^8) table leaves (H >= 3), values in the low 2^H bits of a u64.
+template <int H>
+__device__ __forceinline__ uint64_t dmul_t(uint64_t a, uint64_t b, const uint8_t* tab) {
+	if constexpr (H == 3) {
+		return gf8_mul((uint32_t)a, (uint32_t)b, tab);
+	} else {
+		constexpr int half = 1 << (H - 1);
+		constexpr uint64_t m = (half >= 64) ? ~0ull : ((1ull << half) - 1ull);
+		const uint64_t a0 = a & m, a1 = (a >> half) & m, b0 = b & m, b1 = (b >> half) & m;
+		const uint64_t z0 = dmul_t<H - 1>(a0, b0, tab);
+		const uint64_t z2 = dmul_t<H - 1>(a1, b1, tab);
+		const uint64_t z1 = dmul_t<H - 1>(a0 ^ a1, b0 ^ b1, tab) ^ z0 ^ z2;
+		return (z0 ^ z2) | ((z1 ^ dmul_alpha_u64<H - 1>(z2)) << half);
+	}
+}
+__device__ __forceinline__ uint4 dmul128_t(uint4 a, uint4 b, const uint8_t* tab) {
+	const uint64_t a0 = (uint64_t)a.x | ((uint64_t)a.y << 32), a1 = (uint64_t)a.z | ((uint64_t)a.w << 32);
+	const uint64_t b0 = (uint64_t)b.x | ((uint64_t)b.y << 32), b1 = (uint64_t)b.z | ((uint64_t)b.w << 32);
+	const uint64_t z0 = dmul_t<6>(a0, b0, tab), z2 = dmul_t<6>(a1, b1, tab);
+	const uint64_t z1 = dmul_t<6>(a0 ^ a1, b0 ^ b1, tab) ^ z0 ^ z2;
+	const uint64_t lo = z0 ^ z2, hi = z1 ^ dmul_alpha_u64<6>(z2);
+	return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
 
 template <int H>
 __device__ __forceinline__ uint32_t dmul_alpha(uint32_t a) {
