@@ -31,5 +31,8 @@ def field_kats():
 def dev():
     import torch
     if not torch.cuda.is_available():
+        import binius_ntt_amd as B
+        if B.check_gpu_capabilities():
+            pytest.fail("the HIP engine sees a gfx950 GPU but torch does not (torch.cuda.is_available() is False)")
         pytest.skip("no GPU")
     return torch.device("cuda:0")
