@@ -228,49 +228,48 @@ __device__ __forceinline__ void load_pair(const ScArgs& A, int j, size_t p, int 
 	}
 }
 
+// One (pair, point k) per quad, k fastest: the kmax+1 quads of a pair run side by side, so the
+// pair's columns are read from HBM once and hit in cache for the other points.
 template <int MODE>
 __global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
 	extern __shared__ uint32_t lds[];
 	const int l = threadIdx.x & 3, qw = threadIdx.x >> 2;
 	const Slot S{lds + qw * kQuadWords};
-	const size_t quad0 = (size_t)blockIdx.x * kQuadsPerWG + qw;
-	{  // one interpolation point per grid row
-		const int k = blockIdx.y;
-		uint32_t acc = 0;
-		const size_t p = quad0;
-		if (p < A.n_pairs) {  // one pair per quad (no grid-stride loop: it costs registers)
-			uint32_t emask = 0;
-			for (int j = 0; j < A.d; j++) {
-				// f_j at point k: lo + k (lo + hi), written into the A (j == 0) or B operand
-				uint32_t lo[32], hi[32];
-				load_pair<MODE>(A, j, p, l, lo, hi, emask);
-				if (k == 0) {
-				} else if (k == 1) {
+	uint32_t* accL = lds + kQuadsPerWG * kQuadWords + 128;  // (kMaxD + 1) x 4 words
+	if (threadIdx.x < 4 * (kMaxD + 1)) accL[threadIdx.x] = 0;
+	__syncthreads();
+	const int npts = A.kmax + 1;
+	const size_t item = (size_t)blockIdx.x * kQuadsPerWG + qw;
+	const size_t p = item / npts;
+	const int k = (int)(item % npts);
+	if (p < A.n_pairs) {
+		uint32_t emask = 0;
+		for (int j = 0; j < A.d; j++) {
+			// f_j at point k: lo + k (lo + hi), written into the A (j == 0) or B operand
+			uint32_t lo[32], hi[32];
+			load_pair<MODE>(A, j, p, l, lo, hi, emask);
+			if (k == 0) {
+			} else if (k == 1) {
 #pragma unroll
-					for (int i = 0; i < 32; i++) lo[i] = hi[i];
-				} else {
+				for (int i = 0; i < 32; i++) lo[i] = hi[i];
+			} else {
 #pragma unroll
-					for (int i = 0; i < 32; i++) hi[i] ^= lo[i];
-					mul_small(A.kcol[k], hi, hi);
+				for (int i = 0; i < 32; i++) hi[i] ^= lo[i];
+				mul_small(A.kcol[k], hi, hi);
 #pragma unroll
-					for (int i = 0; i < 32; i++) lo[i] ^= hi[i];
-				}
-				sst(S, (j == 0 ? 0 : 4) + l, lo);
-				if (j > 0) quad_mul<false>(S, nullptr, l);
+				for (int i = 0; i < 32; i++) lo[i] ^= hi[i];
 			}
-			wsync();
-			uint32_t t[32];
-			sld(t, S, l);
-			acc ^= parity_word(t, emask);
-			wsync();
+			sst(S, (j == 0 ? 0 : 4) + l, lo);
+			if (j > 0) quad_mul<false>(S, nullptr, l);
 		}
-		// XOR-reduce over the quads of the wave (lanes with the same limb), then one atomic per limb
-		acc ^= __shfl_xor(acc, 4);
-		acc ^= __shfl_xor(acc, 8);
-		acc ^= __shfl_xor(acc, 16);
-		acc ^= __shfl_xor(acc, 32);
-		if ((threadIdx.x & 63) < 4 && acc) atomicXor(A.acc + 4 * k + l, acc);
+		wsync();
+		uint32_t t[32];
+		sld(t, S, l);
+		const uint32_t acc = parity_word(t, emask);
+		if (acc) atomicXor(accL + 4 * k + l, acc);  // LDS atomic
 	}
+	__syncthreads();
+	if (threadIdx.x < 4 * npts && accL[threadIdx.x]) atomicXor(A.acc + threadIdx.x, accL[threadIdx.x]);
 }
 
 template <int MODE>
@@ -303,7 +302,8 @@ __global__ __launch_bounds__(kScThreads, 2) void sc_fold(ScArgs A) {
 	}
 }
 
-size_t lds_bytes() { return ((size_t)kQuadsPerWG * kQuadWords + 128) * sizeof(uint32_t); }
+// quad slots + the fold's broadcast challenge (128 words) + the messages' accumulators
+size_t lds_bytes() { return ((size_t)kQuadsPerWG * kQuadWords + 128 + 4 * (kMaxD + 1)) * sizeof(uint32_t); }
 
 struct DeviceScope {
 	int prev = -1;
@@ -363,14 +363,14 @@ int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 	if (fold) memcpy(A.r, r, 16);
 	for (int k = 0; k <= kMaxD; k++)
 		for (int a = 0; a < 4; a++) A.kcol[k][a] = (uint32_t)tw_mul((uint64_t)k, 1ull << a, 2);
-	const size_t items = fold ? (size_t)sc->d * A.n_pairs : A.n_pairs;
-	const unsigned rows = fold ? 1u : (unsigned)(A.kmax + 1);  // messages: grid row = point k
-	const size_t grid = (items + kQuadsPerWG - 1) / kQuadsPerWG;  // one item per quad
+	// one item per quad: fold (column, pair), messages (pair, point)
+	const size_t items = fold ? (size_t)sc->d * A.n_pairs : A.n_pairs * (size_t)(A.kmax + 1);
+	const size_t grid = (items + kQuadsPerWG - 1) / kQuadsPerWG;
 	if (!fold) BN_HIP(hipMemsetAsync(sc->acc, 0, sizeof(uint32_t) * 4 * (kMaxD + 1), sc->stream));
 	void* args[] = {&A};
 	const void* fns[2][3] = {{(const void*)sc_messages<0>, (const void*)sc_messages<1>, (const void*)sc_messages<2>},
 							 {(const void*)sc_fold<0>, (const void*)sc_fold<1>, (const void*)sc_fold<2>}};
-	BN_HIP(hipLaunchKernel(fns[fold ? 1 : 0][A.mode], dim3((unsigned)grid, rows), dim3(kScThreads),
+	BN_HIP(hipLaunchKernel(fns[fold ? 1 : 0][A.mode], dim3((unsigned)grid), dim3(kScThreads),
 						   args, lds_bytes(), sc->stream));
 	return BN_OK;
 }

@@ -21,7 +21,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(os.path.dirname(_HERE))  # binius-ntt_amd/
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libbinius_ntt_amd.so")
+LIB_PATH = os.environ.get("BINIUS_NTT_AMD_LIB") or os.path.join(PKG_ROOT, "lib", "libbinius_ntt_amd.so")  # env: A/B experiments
 HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "binius_ntt_amd.h")
 
 BN_OK, BN_ERR_INVALID, BN_ERR_HIP, BN_ERR_UNSUPPORTED, BN_ERR_ALLOC = 0, 1, 2, 3, 4
