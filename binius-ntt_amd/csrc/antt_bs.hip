@@ -198,28 +198,56 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 		const int qu = ((pair >> m) << (m + 1)) | (pair & ((1 << m) - 1));
 		const int qv = qu | (1 << m);
 		const uint32_t w = cu_lds[j] ^ tile_tw(j, qu);
-		uint32_t W[32], V[32], Pr[32];
-#pragma unroll
-		for (int i = 0; i < 32; i++) W[i] = 0u - ((w >> i) & 1u);
 		uint32_t* pu = lds + qu * BLK_WORDS + l * kLimbStride;
 		uint32_t* pv = lds + qv * BLK_WORDS + l * kLimbStride;
+		if constexpr (LAST) {
+			// bottom pass: both rows requested up front (measured faster here; in the upper passes
+			// the extra live row costs more than the hidden latency)
+			uint32_t W[32], V[32], U[32], Pr[32];
 #pragma unroll
-		for (int i = 0; i < 32; i += 4) *(uint4*)(V + i) = *(const uint4*)(pv + i);
-		if (P.dbg & 4) {
+			for (int i = 0; i < 32; i += 4) {
+				*(uint4*)(V + i) = *(const uint4*)(pv + i);
+				*(uint4*)(U + i) = *(const uint4*)(pu + i);
+			}
 #pragma unroll
-			for (int i = 0; i < 32; i++) Pr[i] = V[i] ^ W[i];
+			for (int i = 0; i < 32; i++) W[i] = 0u - ((w >> i) & 1u);
+			__builtin_amdgcn_sched_barrier(0);
+			if (P.dbg & 4) {
+#pragma unroll
+				for (int i = 0; i < 32; i++) Pr[i] = V[i] ^ W[i];
+			} else {
+				mul_tw(ps.field[j], V, W, Pr);  // sub-field circuits reuse W: Pr must not alias it
+			}
+			__builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) {
+				const uint4 u = make_uint4(U[i] ^ Pr[i], U[i + 1] ^ Pr[i + 1], U[i + 2] ^ Pr[i + 2], U[i + 3] ^ Pr[i + 3]);
+				*(uint4*)(pu + i) = u;
+				*(uint4*)(pv + i) = make_uint4(V[i] ^ u.x, V[i + 1] ^ u.y, V[i + 2] ^ u.z, V[i + 3] ^ u.w);
+			}
 		} else {
-			mul_tw(ps.field[j], V, W, Pr);  // sub-field circuits reuse W: Pr must not alias it
-		}
+			// only V and the twiddle are live during the multiply; U is read afterwards
+			uint32_t W[32], V[32], Pr[32];
 #pragma unroll
-		for (int i = 0; i < 32; i += 4) {
-			uint4 u = *(const uint4*)(pu + i);
-			u.x ^= Pr[i];
-			u.y ^= Pr[i + 1];
-			u.z ^= Pr[i + 2];
-			u.w ^= Pr[i + 3];
-			*(uint4*)(pu + i) = u;
-			*(uint4*)(pv + i) = make_uint4(V[i] ^ u.x, V[i + 1] ^ u.y, V[i + 2] ^ u.z, V[i + 3] ^ u.w);
+			for (int i = 0; i < 32; i++) W[i] = 0u - ((w >> i) & 1u);
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) *(uint4*)(V + i) = *(const uint4*)(pv + i);
+			if (P.dbg & 4) {
+#pragma unroll
+				for (int i = 0; i < 32; i++) Pr[i] = V[i] ^ W[i];
+			} else {
+				mul_tw(ps.field[j], V, W, Pr);  // sub-field circuits reuse W: Pr must not alias it
+			}
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) {
+				uint4 u = *(const uint4*)(pu + i);
+				u.x ^= Pr[i];
+				u.y ^= Pr[i + 1];
+				u.z ^= Pr[i + 2];
+				u.w ^= Pr[i + 3];
+				*(uint4*)(pu + i) = u;
+				*(uint4*)(pv + i) = make_uint4(V[i] ^ u.x, V[i + 1] ^ u.y, V[i + 2] ^ u.z, V[i + 3] ^ u.w);
+			}
 		}
 	};
 	const int jlow = max(LAST ? 5 : 0, ps.stop_j);
