@@ -9,7 +9,9 @@ c3  2^20-point GF(2^128) additive NTT, device-resident, elements/s.
 c4  Sumcheck over GF(2^128), 2^N evals, bitsliced input (DATA_IS_TRANSPOSED = true),
     d in {2,3,4}: all N rounds (messages + fold) plus the final messages, device-resident
     columns; evals/s = 2^N / t.  Synthetic evals (numpy PCG64, fixed seed) and challenges.
-c5  one GPU's share of the 256 x 2^20 batched NTT (32 transforms), elements/s.
+c5  one GPU's share of the 256 x 2^20 batched NTT (32 transforms), elements/s; and one GPU's
+    shard (rank 0 of 8) of the 2^28-eval d=3 sumcheck: the sharded rounds up to the endgame
+    gather (the per-round all-gather of (d+2)x16 B partials is not included).
 Every line is one JSON object.
 """
 import argparse
@@ -98,6 +100,30 @@ def c4(dev, out, nvars, ds):
              "hbm_gbps_algorithmic": 3.0 * d * 16 * (1 << nvars) / dt / 1e9})
 
 
+def c5_sumcheck_shard(dev, out, nvars=28, d=3, world=8):
+    import torch
+    import binius_ntt_amd as B
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5C00 + d)
+    ev = torch.randint(-2**31, 2**31 - 1, (4 * (1 << nvars) * d,), dtype=torch.int32, device=dev, generator=g)
+    sc = B.Sumcheck(nvars, d, True, ev, shard=(0, world))  # keeps batches b % 8 == 0
+    del ev
+    torch.cuda.empty_cache()
+    ch = np.random.default_rng(1).integers(0, 2**32, size=(nvars, 4), dtype=np.uint64).astype(np.uint32)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r = 0
+    while not sc.needs_gather():
+        sc.this_round_messages()
+        sc.move_to_next_round(ch[r])
+        r += 1
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    sc.close()
+    out({"config": "c5 (per-GPU share)", "workload": "sumcheck GF(2^128), 2^%d evals, d=%d, shard 0 of %d: %d local rounds"
+         % (nvars, d, world, r), "value": (1 << nvars) / world / dt, "unit": "evals/s (this shard)", "ms": dt * 1e3})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="c2,c3,c4,c5")
@@ -122,6 +148,7 @@ def main():
         c4(dev, out, a.sc_vars, [int(x) for x in a.sc_d.split(",")])
     if "c5" in only:
         ntt_line(dev, out, "c5 (per-GPU share)", 20, 32)
+        c5_sumcheck_shard(dev, out)
     if a.out:
         with open(a.out, "w") as f:
             for d in lines:
