@@ -122,8 +122,10 @@ class Emitter:
                 uses[r] += 1
         self.uses = uses
 
-    def emit(self, input_map, outputs):
-        """input_map: name -> C expression; outputs: list of (C lvalue, node or None)."""
+    def emit(self, input_map, outputs, barrier_every=0):
+        """input_map: name -> C expression; outputs: list of (C lvalue, node or None).
+        barrier_every > 0 inserts a scheduling barrier every that many gates, which keeps the
+        machine scheduler close to the (depth-first, low register pressure) emission order."""
         d = self.d
         live = set()
         stack = [r for _, r in outputs if r is not None]
@@ -182,6 +184,8 @@ class Emitter:
             else:
                 lines.append("const uint32_t %s = %s ^ %s;" % (v, nm(args[0]), nm(args[1])))
             name[n] = v
+            if barrier_every and cnt[0] % barrier_every == 0:
+                lines.append("BN_SCHED_BARRIER();")
         for lv, r in outputs:
             lines.append("%s = %s;" % (lv, "0u" if r is None else nm(r)))
         return lines
@@ -222,6 +226,9 @@ def gen_mulp(h, accumulate=False):
     return pre + body
 
 
+BARRIER_EVERY = int(os.environ.get("BN_GEN_BARRIER_EVERY", "0"))
+
+
 def gen_full(h, accumulate=False):
     """out = a * b (or out ^= a * b), both bitsliced, alias-safe."""
     d = DAG()
@@ -236,7 +243,7 @@ def gen_full(h, accumulate=False):
         imap.update({"o%d" % i: "o%d_" % i for i in range(n)})
         res = [d.xor(r, q) for r, q in zip(res, acc)]
     e = Emitter(d, res)
-    body = e.emit(imap, [("out[%d]" % i, res[i]) for i in range(n)])
+    body = e.emit(imap, [("out[%d]" % i, res[i]) for i in range(n)], BARRIER_EVERY if h <= 5 else 0)
     pre = ["const uint32_t a%d_ = a[%d];" % (i, i) for i in range(n)]
     pre += ["const uint32_t b%d_ = b[%d];" % (i, i) for i in range(n)]
     if accumulate:
@@ -253,7 +260,8 @@ def main():
              "// Bitsliced binary-tower multipliers (Karatsuba tower, gfx950 v_bitop3 fusion).",
              "#pragma once", "#include <hip/hip_runtime.h>", "#include <stdint.h>", "",
              "#define BN_XOR3(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x96)",
-             "#define BN_ANDXOR(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x6a)", "",
+             "#define BN_ANDXOR(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x6a)",
+             "#define BN_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)", "",
              "namespace bn {", ""]
     stats = []
     for h in (2, 3, 4, 5):
