@@ -631,3 +631,69 @@ extern "C" int bn_sumcheck_destroy(bn_sumcheck* sc) {
 	sc_free(sc);
 	return BN_OK;
 }
+
+// ---------------------------------------------------------------------------------------
+// Verifier side
+// ---------------------------------------------------------------------------------------
+namespace {
+
+int composition_eval(bn_sumcheck* sc, const uint32_t* challenges, uint32_t* out) {
+	// folding every column at r_0, r_1, ... (highest variable first) leaves f_j(r); the last
+	// round's "sum" is then prod_j f_j(r)
+	for (int i = 0; i < sc->num_vars; i++) {
+		int rc = bn_sumcheck_move_to_next_round(sc, challenges + 4 * (size_t)i);
+		if (rc != BN_OK) return rc;
+	}
+	uint32_t pts[4 * (kMaxD + 1)];
+	return bn_sumcheck_round_messages(sc, out, pts);
+}
+
+}  // namespace
+
+extern "C" int bn_multilinear_composition_eval(int device, int num_vars, int d, int transposed, const uint32_t* evals,
+											   const uint32_t* challenges, uint32_t* out) {
+	BN_CHECK_ARG(challenges && out, "NULL argument");
+	bn_sumcheck* sc = nullptr;
+	int rc = bn_sumcheck_create(device, num_vars, d, transposed, evals, &sc);
+	if (rc != BN_OK) return rc;
+	rc = composition_eval(sc, challenges, out);
+	bn_sumcheck_destroy(sc);
+	return rc;
+}
+
+extern "C" int bn_multilinear_composition_eval_device(int device, int num_vars, int d, int transposed,
+													  const void* d_evals, const uint32_t* challenges, uint32_t* out) {
+	BN_CHECK_ARG(challenges && out, "NULL argument");
+	bn_sumcheck* sc = nullptr;
+	int rc = bn_sumcheck_create_device(device, num_vars, d, transposed, const_cast<void*>(d_evals), 0, &sc);
+	if (rc != BN_OK) return rc;
+	rc = composition_eval(sc, challenges, out);
+	bn_sumcheck_destroy(sc);
+	return rc;
+}
+
+extern "C" int bn_sumcheck_interpolate(const uint32_t* points, int num_points, const uint32_t* challenge, uint32_t* out) {
+	BN_CHECK_ARG(points && challenge && out, "NULL argument");
+	BN_CHECK_ARG(num_points >= 1 && num_points <= 16, "num_points must be in [1, 16]");
+	auto ld = [](const uint32_t* w) {
+		return bn::u128p{(uint64_t)w[0] | ((uint64_t)w[1] << 32), (uint64_t)w[2] | ((uint64_t)w[3] << 32)};
+	};
+	const bn::u128p r = ld(challenge);
+	bn::u128p acc{0, 0};
+	for (int i = 0; i < num_points; i++) {
+		bn::u128p t = ld(points + 4 * i);
+		for (int j = 0; j < num_points; j++) {
+			if (j == i) continue;
+			t = bn::tw_mul128(t, bn::u128p{r.lo ^ (uint64_t)j, r.hi});
+			// 1 / (i - j) lies in GF(2^4) (inverse_at_interpolation_point, tower_7_mul.cu:22-24)
+			t = bn::tw_mul128(t, bn::u128p{bn::tw_inv((uint64_t)(i ^ j), 2), 0});
+		}
+		acc.lo ^= t.lo;
+		acc.hi ^= t.hi;
+	}
+	out[0] = (uint32_t)acc.lo;
+	out[1] = (uint32_t)(acc.lo >> 32);
+	out[2] = (uint32_t)acc.hi;
+	out[3] = (uint32_t)(acc.hi >> 32);
+	return BN_OK;
+}

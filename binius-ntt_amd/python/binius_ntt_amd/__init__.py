@@ -72,6 +72,9 @@ def lib():
         "bn_sumcheck_export_shard": (i32, [vp, u32p, sz]),
         "bn_sumcheck_import_gathered": (i32, [vp, u32p, sz, i32]),
         "bn_sumcheck_destroy": (i32, [vp]),
+        "bn_multilinear_composition_eval": (i32, [i32, i32, i32, i32, u32p, u32p, u32p]),
+        "bn_multilinear_composition_eval_device": (i32, [i32, i32, i32, i32, vp, u32p, u32p]),
+        "bn_sumcheck_interpolate": (i32, [u32p, i32, u32p, u32p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -313,3 +316,33 @@ class Sumcheck:
             self.close()
         except Exception:
             pass
+
+
+def _u32p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+
+
+def evaluate_multilinear_composition(evals, num_vars, composition_size, data_is_transposed, challenges, device=0):
+    """evaluate_multilinear_composition (src/ulvt/sumcheck/test/verifier.cu:88-107) on the GPU:
+    prod_j f_j(r) for the columns in `evals` (numpy host array or torch device tensor)."""
+    ch = np.ascontiguousarray(challenges, dtype=np.uint32).reshape(-1)
+    out = np.zeros(4, np.uint32)
+    if isinstance(evals, np.ndarray):
+        ev = np.ascontiguousarray(evals, dtype=np.uint32).reshape(-1)
+        _check(lib().bn_multilinear_composition_eval(device, num_vars, composition_size, 1 if data_is_transposed else 0,
+                                                     _u32p(ev), _u32p(ch), _u32p(out)))
+    else:
+        _check(lib().bn_multilinear_composition_eval_device(device, num_vars, composition_size,
+                                                            1 if data_is_transposed else 0, _ptr(evals), _u32p(ch),
+                                                            _u32p(out)))
+    return out
+
+
+def evaluate_univariate_given_points(challenge, points):
+    """evaluate_univariate_given_points (verifier.cu:9-31): Lagrange interpolation through
+    (k, points[k]) evaluated at `challenge` (4-word GF(2^128) values)."""
+    p = np.ascontiguousarray(points, dtype=np.uint32).reshape(-1)
+    c = np.ascontiguousarray(challenge, dtype=np.uint32).reshape(4)
+    out = np.zeros(4, np.uint32)
+    _check(lib().bn_sumcheck_interpolate(_u32p(p), p.size // 4, _u32p(c), _u32p(out)))
+    return out

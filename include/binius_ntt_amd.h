@@ -147,6 +147,25 @@ int bn_sumcheck_export_shard(const bn_sumcheck* sc, uint32_t* out, size_t out_wo
 int bn_sumcheck_import_gathered(bn_sumcheck* sc, const uint32_t* words, size_t n_words, int world);
 int bn_sumcheck_destroy(bn_sumcheck* sc);
 
+/* ------------------------------------------------------------------------------------
+ * Verifier side of the sumcheck (src/ulvt/sumcheck/test/verifier.cu)
+ * ------------------------------------------------------------------------------------ */
+/* Replaces evaluate_multilinear_composition(evals, challenges, num_vars, composition_size)
+ * (verifier.cu:88-107, with evaluate_multilinear_given_point :33-86 and lagrange_basis_eval,
+ * kernel/verifier_kernel.cu:4-37): out = prod_j sum_x f_j(x) prod_v (x_v ? r[n-1-v] : 1 + r[n-1-v]),
+ * i.e. every column folded at the challenges (highest variable first), multiplied together.
+ * Computed on `device` by the sumcheck fold kernels. evals as bn_sumcheck_create (host memory,
+ * compact or bitsliced); challenges: num_vars x 4 words. Synchronous. */
+int bn_multilinear_composition_eval(int device, int num_vars, int composition_size, int data_is_transposed,
+                                    const uint32_t* evals, const uint32_t* challenges, uint32_t* out);
+/* Same with the columns already in device memory (left untouched). */
+int bn_multilinear_composition_eval_device(int device, int num_vars, int composition_size, int data_is_transposed,
+                                           const void* d_evals, const uint32_t* challenges, uint32_t* out);
+/* Replaces evaluate_univariate_given_points(challenge, points, num_points) (verifier.cu:9-31):
+ * Lagrange interpolation through (k, points[k]), k = 0..num_points-1 (tower elements), evaluated
+ * at `challenge`. Host arithmetic; 1 <= num_points <= 16. */
+int bn_sumcheck_interpolate(const uint32_t* points, int num_points, const uint32_t* challenge, uint32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -14,6 +14,7 @@
 #include "finite_fields/binary_tower.hpp"
 #include "ntt/additive_ntt.hpp"
 #include "sumcheck/sumcheck.hpp"
+#include "sumcheck/verifier.hpp"
 #include "utils/bitslicing.hpp"
 #include "../../oracle/oracle.h"
 
@@ -136,7 +137,8 @@ static void sumcheck_protocol() {
 		std::array<uint32_t, 4> ch;
 		for (auto& w : ch) w = (uint32_t)g();
 		std::memcpy(&challenges[4 * round], ch.data(), 16);
-		// evaluate_univariate_given_points: Lagrange through (k, points[k]), k = 0..D
+		// evaluate_univariate_given_points: Lagrange through (k, points[k]), k = 0..D, once with the
+		// host field policy and once through the library
 		const u128 r = big(ch.data());
 		u128 acc = 0;
 		for (uint32_t i = 0; i <= D; i++) {
@@ -148,6 +150,7 @@ static void sumcheck_protocol() {
 			}
 			acc ^= t;
 		}
+		ok = ok && acc == evaluate_univariate_given_points(r, (const u128*)points.data(), D + 1);
 		claim = acc;
 		s.move_to_next_round(ch);
 	}
@@ -158,6 +161,10 @@ static void sumcheck_protocol() {
 	uint32_t brute[4];
 	orc_multilinear_composition(compact.data(), N, D, challenges.data(), brute);
 	ok = ok && big(brute) == claim;
+	// the library's own verifier helpers (verifier.cu:9-31, 88-107)
+	const __uint128_t gpu_claim = evaluate_multilinear_composition((const __uint128_t*)compact.data(),
+																   (const __uint128_t*)challenges.data(), N, D);
+	ok = ok && gpu_claim == claim;
 	char what[96];
 	std::snprintf(what, sizeof(what), "Sumcheck<%u, %u, %s> protocol checks + final claim", N, D, T ? "true" : "false");
 	check(ok, what);

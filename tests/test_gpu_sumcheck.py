@@ -132,3 +132,37 @@ def test_sumcheck_errors(dev):
         B.Sumcheck(4, 2, True, _rand(4 * 16 * 2, 1))  # bitsliced input below one batch
     with pytest.raises(B.BnError):
         B.Sumcheck(6, 9, False, _rand(4 * 64 * 9, 1))  # composition size above 8
+
+
+@pytest.mark.parametrize("n,d,transposed", [(1, 1, 0), (4, 3, 0), (5, 2, 1), (9, 3, 0), (12, 4, 1), (13, 1, 1)])
+def test_multilinear_composition_eval_matches_oracle(n, d, transposed, dev):
+    # evaluate_multilinear_composition (verifier.cu:88-107) on the GPU vs the oracle
+    ev, ch = _case(n, d, 900 + 10 * n + d)
+    inp = O.bitslice128(ev) if transposed else ev
+    want = O.multilinear_composition(ev, n, d, ch)
+    assert np.array_equal(B.evaluate_multilinear_composition(inp, n, d, transposed, ch), want)
+    import torch
+    t = torch.from_numpy(inp.view(np.int32)).to(dev)
+    assert np.array_equal(B.evaluate_multilinear_composition(t, n, d, transposed, ch), want)
+    assert np.array_equal(t.cpu().numpy().view(np.uint32), inp)  # device input untouched
+
+
+def test_full_protocol_with_gpu_verifier(dev):
+    # test.cu:13-101 with every verifier step on this library: interpolation on the host,
+    # the final brute-force claim on the GPU
+    n, d = 18, 3
+    ev, ch = _case(n, d, 31337)
+    bs = O.bitslice128(ev)
+    sc = B.Sumcheck(n, d, True, bs)
+    claim = None
+    for r in range(n):
+        s, p = sc.this_round_messages()
+        if r > 0:
+            assert np.array_equal(s, claim)
+        assert np.array_equal(s, p[0] ^ p[1])
+        claim = B.evaluate_univariate_given_points(ch[r], p)
+        sc.move_to_next_round(ch[r])
+    s, _ = sc.this_round_messages()
+    assert np.array_equal(s, claim)
+    assert np.array_equal(B.evaluate_multilinear_composition(bs, n, d, True, ch), claim)
+    sc.close()
