@@ -153,8 +153,10 @@ int launch_v0(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, hipStre
 	int hi = log_h;
 	bool first = true;
 	int kind = 0;
+	// balanced passes of <= kTileLog stages (an unbalanced tail would launch 2-point tiles)
+	const int passes = (log_h + kTileLog - 1) / kTileLog;
 	while (hi > 0) {
-		const int k = std::min(hi, kTileLog);
+		const int k = (hi + (passes - kind) - 1) / (passes - kind);
 		const int lo = hi - k;
 		const int c = std::min(lo, kTileLog - k);
 		V0Params p{d_in, d_out, plan->s_dev, plan->width, log_h, plan->log_rate, lo, k, c, first ? 1 : 0};
@@ -320,6 +322,22 @@ extern "C" int bn_antt_plan_query(const bn_antt_plan* p, int what, int64_t* valu
 		case 4: *value = p->variant; break;
 		default: BN_FAIL(BN_ERR_INVALID, "unknown query %d", what);
 	}
+	return BN_OK;
+}
+
+extern "C" int bn_antt_plan_set_variant(bn_antt_plan* p, int variant) {
+	BN_CHECK_ARG(p != nullptr, "plan is NULL");
+	BN_CHECK_ARG(variant == 0 || variant == 1, "variant must be 0 or 1");
+	if (variant == 1 && !bs_supports(p)) BN_FAIL(BN_ERR_UNSUPPORTED, "variant 1 needs log_h >= 12");
+	if (variant == 1 && p->variant != 1) {
+		int prev = 0;
+		hipGetDevice(&prev);
+		BN_HIP(hipSetDevice(p->device));
+		const int rc = bs_prepare(p);
+		hipSetDevice(prev);
+		if (rc != BN_OK) return rc;
+	}
+	p->variant = variant;
 	return BN_OK;
 }
 

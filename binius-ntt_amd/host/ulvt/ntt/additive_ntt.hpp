@@ -42,6 +42,9 @@ public:
 		ulvt::bn_check(bn_antt_forward_device(plan, d_in, d_out, batch, stream));
 	}
 
+	// 0: compact tiles, per-butterfly twiddles; 1: bitsliced tiles (default for log_h >= 12)
+	void set_variant(int variant) { ulvt::bn_check(bn_antt_plan_set_variant(plan, variant)); }
+
 	const AdditiveNTTConf<T, P>& conf() const { return ntt_conf; }
 
 private:

@@ -43,6 +43,14 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("libbinius_ntt_amd.so not built (run `make -C binius-ntt_amd` or __graft_entry__.build())")
+    # One HIP runtime per process: torch bundles its own libamdhip64 with the same SONAME as
+    # ROCm's. If this library were loaded first it would pull in ROCm's copy and torch (which
+    # this package uses for device buffers and streams) would then find no GPU. Import torch
+    # first so that its runtime is the one both share.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, sz, i32, u32p = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)
     sig = {
@@ -55,6 +63,7 @@ def lib():
         "bn_antt_forward_device": (i32, [vp, vp, vp, sz, vp]),
         "bn_antt_get_subspace_evals": (i32, [vp, u32p, sz]),
         "bn_antt_plan_query": (i32, [vp, i32, ctypes.POINTER(ctypes.c_int64)]),
+        "bn_antt_plan_set_variant": (i32, [vp, i32]),
         "bn_antt_set_event_timing": (i32, [vp, i32]),
         "bn_antt_get_event_timing": (i32, [vp, ctypes.POINTER(ctypes.c_float), i32, ctypes.POINTER(i32)]),
         "bn_gf128_mul_device": (i32, [vp, vp, vp, sz, vp]),
@@ -224,6 +233,10 @@ class AdditiveNTT:
         v = ctypes.c_int64()
         _check(lib().bn_antt_plan_query(self._plan, 4, ctypes.byref(v)))
         return v.value
+
+    def set_variant(self, variant):
+        """0: compact tiles, per-butterfly twiddles; 1: bitsliced tiles (default for log_h >= 12)."""
+        _check(lib().bn_antt_plan_set_variant(self._plan, variant))
 
     def set_event_timing(self, enable):
         _check(lib().bn_antt_set_event_timing(self._plan, 1 if enable else 0))

@@ -75,6 +75,11 @@ int bn_antt_get_subspace_evals(const bn_antt_plan* plan, uint32_t* out, size_t o
 
 /* Plan introspection: 0 log_h, 1 log_rate, 2 field_bits, 3 device, 4 kernel variant. */
 int bn_antt_plan_query(const bn_antt_plan* plan, int what, int64_t* value);
+/* Kernel selection, the analogue of choosing AdditiveNTT vs ModifiedAdditiveNTT
+ * (src/ulvt/ntt/modified_antt.cuh:223-427, benchmark_antt.cu): 0 = compact tiles with the twiddle
+ * recomputed per butterfly from the subspace table (the reference kernel's scheme), 1 = bitsliced
+ * tiles with host-tabulated twiddle contributions (default when log_h >= 12). */
+int bn_antt_plan_set_variant(bn_antt_plan* plan, int variant);
 
 /* Profiling hook for bench.py: records hipEvents around every kernel launch of the next
  * bn_antt_forward_device call on its stream and returns per-launch-kind mean durations. */

@@ -23,9 +23,34 @@ def _build():
     subprocess.check_call(cmd)
 
 
+BENCH = os.path.join(ROOT, "tests", "cpp", "build", "benchmark_antt")
+
+
+def _build_bench():
+    os.makedirs(os.path.dirname(BENCH), exist_ok=True)
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-I", os.path.join(ROOT, "include"),
+                           "-I", os.path.join(ROOT, "binius-ntt_amd", "host", "ulvt"),
+                           os.path.join(ROOT, "tools", "cpp", "benchmark_antt.cpp"), "-o", BENCH,
+                           "-L", LIBDIR, "-lbinius_ntt_amd", "-L", ORACLE, "-loracle",
+                           "-Wl,-rpath," + LIBDIR, "-Wl,-rpath," + ORACLE, "-Wl,--allow-shlib-undefined"])
+
+
 def test_cpp_mirror_builds_against_the_c_abi():
     _build()
     assert os.path.exists(BIN)
+    _build_bench()
+    assert os.path.exists(BENCH)
+
+
+@pytest.mark.gpu
+def test_benchmark_antt_harness_all_pass(ntt_md5, tmp_path):
+    # the benchmark_antt.cu table (both kernel variants, every row checked against the MD5 table)
+    _build_bench()
+    hashes = tmp_path / "hashes.txt"
+    hashes.write_text("".join("%d %s\n" % (i, h) for i, h in enumerate(ntt_md5["0"]) if h))
+    p = subprocess.run([BENCH, str(hashes), "20"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "Modified tests passed: 20/20" in p.stdout
 
 
 @pytest.mark.gpu
