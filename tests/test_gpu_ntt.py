@@ -23,9 +23,10 @@ def test_capabilities():
     assert B.check_gpu_capabilities(), B.lib().bn_last_error()
 
 
-@pytest.mark.parametrize("log_h", list(range(1, 25)))
+@pytest.mark.parametrize("log_h", list(range(1, 25)) + [pytest.param(h, marks=pytest.mark.slow) for h in range(25, 29)])
 def test_gf32_r0_reference_md5(ntt_md5, log_h, dev):
-    # exactly the reference's run_and_check_additive_ntt(log_h, 0) (test_ntt.cu:191-217)
+    # exactly the reference's run_and_check_additive_ntt(log_h, 0) (test_ntt.cu:191-217), up to
+    # the largest size the reference runs by default (28; 29-30 are its [slow] cases)
     x = O.mt_fill(0xDEADBEEF + log_h, 1 << log_h)
     ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(5)))
     inp = B.NTTData(1 << log_h, B.DataOrder.IN_ORDER, 32, x)
@@ -35,7 +36,7 @@ def test_gf32_r0_reference_md5(ntt_md5, log_h, dev):
     assert O.md5(out.data) == ntt_md5["0"][log_h]
 
 
-@pytest.mark.parametrize("log_h", list(range(1, 23)))
+@pytest.mark.parametrize("log_h", list(range(1, 23)) + [pytest.param(h, marks=pytest.mark.slow) for h in range(23, 28)])
 def test_gf32_r2_reference_md5(ntt_md5, log_h, dev):
     x = O.mt_fill(0xDEADBEEF + log_h + 2, 1 << log_h)
     ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 2, B.FanPaarTowerField(5)))
