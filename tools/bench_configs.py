@@ -100,6 +100,29 @@ def c4(dev, out, nvars, ds):
              "hbm_gbps_algorithmic": 3.0 * d * 16 * (1 << nvars) / dt / 1e9})
 
 
+def c5_sumcheck_single(dev, out, nvars=28, d=3):
+    """The whole 2^28-eval d=3 sumcheck on ONE GPU (12.9 GB of columns, fits in 288 GB)."""
+    import torch
+    import binius_ntt_amd as B
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5C00 + d)
+    ev = torch.randint(-2**31, 2**31 - 1, (4 * (1 << nvars) * d,), dtype=torch.int32, device=dev, generator=g)
+    ch = np.random.default_rng(1).integers(0, 2**32, size=(nvars, 4), dtype=np.uint64).astype(np.uint32)
+    sc = B.Sumcheck(nvars, d, True, ev)
+    del ev
+    torch.cuda.empty_cache()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for r in range(nvars):
+        sc.this_round_messages()
+        sc.move_to_next_round(ch[r])
+    sc.this_round_messages()
+    dt = time.perf_counter() - t0
+    sc.close()
+    out({"config": "c5 (1 GPU, whole problem)", "workload": "sumcheck GF(2^128), 2^%d evals, d=%d, bitsliced input"
+         % (nvars, d), "value": (1 << nvars) / dt, "unit": "evals/s", "ms": dt * 1e3})
+
+
 def c5_sumcheck_shard(dev, out, nvars=28, d=3, world=8):
     import torch
     import binius_ntt_amd as B
@@ -149,6 +172,7 @@ def main():
     if "c5" in only:
         ntt_line(dev, out, "c5 (per-GPU share)", 20, 32)
         c5_sumcheck_shard(dev, out)
+        c5_sumcheck_single(dev, out)
     if a.out:
         with open(a.out, "w") as f:
             for d in lines:
