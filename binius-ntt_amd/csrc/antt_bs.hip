@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <vector>
 
 #include "antt_plan.hpp"
@@ -61,9 +62,12 @@ struct BsPass {
 struct BsParams {
 	const uint32_t* src;
 	uint32_t* dst;
+	size_t ntiles;  // tiles of the pass; the (persistent) grid may be smaller
 	int log_h, log_rate;
+	unsigned long long* trace;  // BN_TRACE=1: per-wave phase timestamps (dev tool)
 	int dbg;  // timing experiments only (BN_DEBUG_FLAGS): 1 no loads, 2 no stores, 4 no multiplies,
-	          // 8 no stage barriers, 16 no in-word stages, 32 no tile-bit stages
+	          // 8 no stage barriers, 16 no in-word stages, 32 no tile-bit stages,
+	          // 64 no lgkmcnt wait between stages
 	BsPass p;
 };
 
@@ -88,12 +92,14 @@ __host__ __device__ constexpr uint32_t lane_mask(int j) {
 }
 
 // out = w*x for 32 bitsliced GF(2^32) limbs (alias-safe: out may be x). W holds bit i of each
-// lane's twiddle in word i; `field` (uniform per stage) selects the sub-field circuit.
+// lane's twiddle in word i; `field` (uniform per stage) selects the sub-field circuit, FMAX (the
+// largest field of the pass) removes the circuits a pass never uses.
+template <int FMAX>
 __device__ __forceinline__ void mul_tw(int field, const uint32_t* x, const uint32_t* W, uint32_t* out) {
-	if (field <= 8) {
+	if (FMAX <= 8 || field <= 8) {
 #pragma unroll
 		for (int g = 0; g < 4; g++) bsm3_mul(x + 8 * g, W, out + 8 * g);
-	} else if (field <= 16) {
+	} else if (FMAX <= 16 || field <= 16) {
 #pragma unroll
 		for (int g = 0; g < 2; g++) bsm4_mul(x + 16 * g, W, out + 16 * g);
 	} else {
@@ -101,191 +107,256 @@ __device__ __forceinline__ void mul_tw(int field, const uint32_t* x, const uint3
 	}
 }
 
-template <int L, int ROLE>
+// LDS image of a tile: one plane per limb, block q of limb l at l*kPlane + q*kLimbStride (stride 36
+// words: 16 consecutive blocks of one plane hit 16 distinct 4-bank groups, so a wave's
+// ds_read_b128 over consecutive blocks is conflict-free).
+constexpr int kPlane = kTileBlocks * kLimbStride;
+constexpr int kLoads = kTileBlocks * 8 / 64;  // 16-byte global loads per lane per tile
+
+// Stage-to-stage ordering inside one wave: a wave's LDS operations execute in order, so only the
+// compiler must not move accesses across this point (the wait also bounds the LDS queue).
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// One pass over every tile. Without PF a workgroup transforms tile blockIdx.x. With PF the grid
+// is persistent (workgroup b takes tiles b, b + grid, ...) and the next tile's global loads are
+// issued into registers right after the current tile reaches LDS, so they are in flight during
+// the stages instead of exposed at the start of the next tile.
+template <int L, int ROLE, int FMAX, bool PF>
 __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 	extern __shared__ uint32_t lds[];
-	constexpr int BLK_WORDS = L * kLimbStride;
 	constexpr int NT = 64 * L;
 	constexpr bool IN_COMPACT = ROLE == ROLE_FIRST || ROLE == ROLE_SINGLE;
 	constexpr bool LAST = ROLE == ROLE_LAST || ROLE == ROLE_SINGLE;  // bottom pass, compact out
-	uint32_t* cu_lds = lds + kTileBlocks * BLK_WORDS;                // workgroup part of each twiddle
 	const BsPass& ps = P.p;
 	const int tid = threadIdx.x;
+	// wave w owns limb w of the tile for every stage: the waves never wait for each other
+	// between stages (the four GF(2^32) limb transforms share only their twiddles)
+	const int l = tid >> 6, lane = tid & 63;
+	uint32_t* plane = lds + l * kPlane;
+	uint32_t* cu_w = lds + L * kPlane + l * kMaxStages;  // this wave's copy of the uniform twiddle parts
 	const size_t n = (size_t)1 << P.log_h;
+	const bool TR = P.trace != nullptr;
+	unsigned long long tr[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // load, block, in-word, store, tiles, pre, mul, post
+	auto ts = [&]() -> unsigned long long {
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+		return __builtin_amdgcn_s_memtime();
+	};
 
-	// ---- workgroup -> (batch, coset, outer bits)
-	const size_t bid = blockIdx.x;
-	const size_t outer = bid & (((size_t)1 << ps.n_outer) - 1);
-	const size_t rest = bid >> ps.n_outer;
-	const int coset = (int)(rest & ((1u << P.log_rate) - 1));
-	const size_t batch = rest >> P.log_rate;
-	size_t outer_off = 0;
-	for (int m = 0; m < ps.n_outer; m++) outer_off |= ((outer >> m) & 1) << ps.ob[m];
 	auto tile_off = [&](int q) -> size_t {
 		size_t off = 0;
 #pragma unroll
 		for (int m = 0; m < kBlkBits; m++) off |= (size_t)((q >> m) & 1) << ps.bb[m];
 		return off;
 	};
-	uint32_t* dst = P.dst + (((batch << P.log_rate) + (size_t)coset) * n) * L;
-	const uint32_t* src = IN_COMPACT ? (P.src + batch * n * L) : dst;
-
-	// ---- load tile into LDS (coalesced 16-byte loads, all issued before the first LDS write;
-	//      compact input is split by limb)
-	constexpr int LOADS = kTileBlocks * 8 * L / NT;
-	uint4 gbuf[LOADS];
+	// tile -> (outer bits, coset, batch) -> addresses
+	size_t outer, outer_off;
+	int coset;
+	uint32_t* dst;
+	const uint32_t* src;
+	auto geo = [&](size_t t, size_t& o, size_t& ooff, int& c, uint32_t*& d, const uint32_t*& s) {
+		o = t & (((size_t)1 << ps.n_outer) - 1);
+		const size_t rest = t >> ps.n_outer;
+		c = (int)(rest & ((1u << P.log_rate) - 1));
+		const size_t batch = rest >> P.log_rate;
+		ooff = 0;
+		for (int m = 0; m < ps.n_outer; m++) ooff |= ((o >> m) & 1) << ps.ob[m];
+		d = P.dst + (((batch << P.log_rate) + (size_t)c) * n) * L;
+		s = IN_COMPACT ? (P.src + batch * n * L) : d;
+	};
+	uint4 gbuf[kLoads];
+	auto issue = [&](const uint32_t* s, size_t ooff) {
 #pragma unroll
-	for (int r = 0; r < LOADS; r++) {
-		const int u = tid + r * NT;
-		const int q = u / (8 * L), j = u % (8 * L);
-		if (P.dbg & 1)
-			gbuf[r] = make_uint4(u, j, q, tid);
-		else
-			gbuf[r] = ld_stream(src + (outer_off | tile_off(q)) * L + 4 * j);
-	}
-	// workgroup-uniform twiddle part of every stage (outer + coset bits), one lane per stage
-	if (tid < ps.k) {
-		uint32_t c = 0;
-		for (int m = 0; m < ps.n_outer; m++) c ^= ps.two[tid][m] & (0u - (uint32_t)((outer >> m) & 1));
-		for (int b = 0; b < P.log_rate; b++) c ^= ps.twc[tid][b] & (0u - (uint32_t)((coset >> b) & 1));
-		cu_lds[tid] = c;
-	}
-#pragma unroll
-	for (int r = 0; r < LOADS; r++) {
-		const int u = tid + r * NT;
-		const int q = u / (8 * L), j = u % (8 * L);
-		const uint4 g = gbuf[r];
-		uint32_t* b = lds + q * BLK_WORDS;
-		if (IN_COMPACT) {
-			const uint32_t w[4] = {g.x, g.y, g.z, g.w};
-#pragma unroll
-			for (int t = 0; t < 4; t++) {
-				const int word = 4 * j + t;
-				b[(word % L) * kLimbStride + word / L] = w[t];
+		for (int r = 0; r < kLoads; r++) {
+			if (IN_COMPACT) {
+				// compact elements: 16-byte loads, 8*L lanes per 32-element block
+				const int u = tid + r * NT;
+				const int q = u / (8 * L), j = u % (8 * L);
+				gbuf[r] = (P.dbg & 1) ? make_uint4(u, j, q, tid) : ld_stream(s + (ooff | tile_off(q)) * L + 4 * j);
+			} else {
+				// bitsliced: limb l of block q is 128 contiguous bytes, each wave loads its own plane
+				const int u = lane + r * 64;
+				const int q = u >> 3, j = u & 7;
+				gbuf[r] = (P.dbg & 1) ? make_uint4(u, j, q, tid) : ld_stream(s + (ooff | tile_off(q)) * L + 32 * l + 4 * j);
 			}
-		} else {
-			const int l = (4 * j) / 32, i = (4 * j) % 32;
-			*(uint4*)(b + l * kLimbStride + i) = g;
 		}
-	}
-	__syncthreads();
-	if (IN_COMPACT) {
-		for (int u = tid; u < kTileBlocks * L; u += NT) {
-			uint32_t* x = lds + (u / L) * BLK_WORDS + (u % L) * kLimbStride;
-			uint32_t r[32];
-#pragma unroll
-			for (int i = 0; i < 32; i += 4) *(uint4*)(r + i) = *(const uint4*)(x + i);
-			transpose32(r);
-#pragma unroll
-			for (int i = 0; i < 32; i += 4) *(uint4*)(x + i) = *(const uint4*)(r + i);
-		}
-		__syncthreads();
-	}
+	};
 
-	const int l = tid % L;
 	auto tile_tw = [&](int j, int q) -> uint32_t {
 		uint32_t w = 0;
 #pragma unroll
-		for (int m = 0; m < kBlkBits; m++) w ^= ps.twt[j][m] & (0u - (uint32_t)((q >> m) & 1));
+		for (int m = 0; m < kBlkBits; m++) w ^= ps.twt[j][m] & (uint32_t)__builtin_amdgcn_sbfe(q, m, 1);
 		return w;
 	};
 
-	// ---- tile-bit stages (index bits >= 5), high to low, through LDS. One thread per
-	// (block pair, limb); only V and the twiddle are live during the multiply. Consecutive lanes
-	// take consecutive pairs, which keeps the padded LDS rows free of bank conflicts.
+	// ---- tile-bit stages (index bits >= 5), high to low. Lane = block pair of the wave's limb;
+	// only V and the twiddle are live during the multiply, U is read afterwards.
 	auto block_stage = [&](int j, int pair) {
+		unsigned long long t_a = TR ? ts() : 0;
 		const int m = ps.stage_m[j];
 		const int qu = ((pair >> m) << (m + 1)) | (pair & ((1 << m) - 1));
 		const int qv = qu | (1 << m);
-		const uint32_t w = cu_lds[j] ^ tile_tw(j, qu);
-		uint32_t* pu = lds + qu * BLK_WORDS + l * kLimbStride;
-		uint32_t* pv = lds + qv * BLK_WORDS + l * kLimbStride;
-		if constexpr (LAST) {
-			// bottom pass: both rows requested up front (measured faster here; in the upper passes
-			// the extra live row costs more than the hidden latency)
-			uint32_t W[32], V[32], U[32], Pr[32];
+		const uint32_t w = cu_w[j] ^ tile_tw(j, qu);
+		uint32_t* pu = plane + qu * kLimbStride;
+		uint32_t* pv = plane + qv * kLimbStride;
+		uint32_t W[32], V[32], Pr[32], U[32];
 #pragma unroll
-			for (int i = 0; i < 32; i += 4) {
-				*(uint4*)(V + i) = *(const uint4*)(pv + i);
-				*(uint4*)(U + i) = *(const uint4*)(pu + i);
-			}
+		for (int i = 0; i < 32; i += 4) *(uint4*)(V + i) = *(const uint4*)(pv + i);
+		// with the small GF(2^8) circuits there are registers for U: request it before the multiply
+		if (FMAX <= 8) {
 #pragma unroll
-			for (int i = 0; i < 32; i++) W[i] = 0u - ((w >> i) & 1u);
-			__builtin_amdgcn_sched_barrier(0);
-			if (P.dbg & 4) {
+			for (int i = 0; i < 32; i += 4) *(uint4*)(U + i) = *(const uint4*)(pu + i);
+		}
 #pragma unroll
-				for (int i = 0; i < 32; i++) Pr[i] = V[i] ^ W[i];
-			} else {
-				mul_tw(ps.field[j], V, W, Pr);  // sub-field circuits reuse W: Pr must not alias it
-			}
-			__builtin_amdgcn_sched_barrier(0);
+		for (int i = 0; i < 32; i++) W[i] = (uint32_t)__builtin_amdgcn_sbfe(w, i, 1);
+		if (TR) {
+			const unsigned long long t = ts();
+			tr[5] += t - t_a;
+			t_a = t;
+		}
+		if (P.dbg & 4) {
 #pragma unroll
-			for (int i = 0; i < 32; i += 4) {
-				const uint4 u = make_uint4(U[i] ^ Pr[i], U[i + 1] ^ Pr[i + 1], U[i + 2] ^ Pr[i + 2], U[i + 3] ^ Pr[i + 3]);
-				*(uint4*)(pu + i) = u;
-				*(uint4*)(pv + i) = make_uint4(V[i] ^ u.x, V[i + 1] ^ u.y, V[i + 2] ^ u.z, V[i + 3] ^ u.w);
-			}
+			for (int i = 0; i < 32; i++) Pr[i] = V[i] ^ W[i];
 		} else {
-			// only V and the twiddle are live during the multiply; U is read afterwards
-			uint32_t W[32], V[32], Pr[32];
+			__builtin_amdgcn_sched_barrier(0);
+			mul_tw<FMAX>(ps.field[j], V, W, Pr);  // sub-field circuits reuse W: Pr must not alias it
+			__builtin_amdgcn_sched_barrier(0);
+		}
+		if (TR) {
+			uint32_t acc = 0;
 #pragma unroll
-			for (int i = 0; i < 32; i++) W[i] = 0u - ((w >> i) & 1u);
+			for (int i = 0; i < 32; i++) acc ^= Pr[i];
+			asm volatile("" ::"v"(acc));
+			const unsigned long long t = ts();
+			tr[6] += t - t_a;
+			t_a = t;
+		}
 #pragma unroll
-			for (int i = 0; i < 32; i += 4) *(uint4*)(V + i) = *(const uint4*)(pv + i);
-			if (P.dbg & 4) {
+		for (int i = 0; i < 32; i += 4) {
+			uint4 u = FMAX <= 8 ? *(const uint4*)(U + i) : *(const uint4*)(pu + i);
+			u.x ^= Pr[i];
+			u.y ^= Pr[i + 1];
+			u.z ^= Pr[i + 2];
+			u.w ^= Pr[i + 3];
+			*(uint4*)(pu + i) = u;
+			*(uint4*)(pv + i) = make_uint4(V[i] ^ u.x, V[i + 1] ^ u.y, V[i + 2] ^ u.z, V[i + 3] ^ u.w);
+		}
+		if (TR) tr[7] += ts() - t_a;
+	};
+
+	size_t tile = blockIdx.x;
+	geo(tile, outer, outer_off, coset, dst, src);
+	if (PF) issue(src, outer_off);
+	for (;;) {
+		unsigned long long t0 = TR ? ts() : 0;
+		// the previous tile's cross-plane LDS readers (compact store) / writers (compact load)
+		// are done before this tile's planes are overwritten
+		if (IN_COMPACT || LAST) __syncthreads();
+		if (!PF) issue(src, outer_off);
+
+		// workgroup-uniform twiddle part of every stage (outer + coset bits), one lane per stage
+		if (lane < ps.k) {
+			uint32_t c = 0;
+			for (int m = 0; m < ps.n_outer; m++) c ^= ps.two[lane][m] & (0u - (uint32_t)((outer >> m) & 1));
+			for (int b = 0; b < P.log_rate; b++) c ^= ps.twc[lane][b] & (0u - (uint32_t)((coset >> b) & 1));
+			cu_w[lane] = c;
+		}
+
+		// ---- tile into LDS
 #pragma unroll
-				for (int i = 0; i < 32; i++) Pr[i] = V[i] ^ W[i];
+		for (int r = 0; r < kLoads; r++) {
+			const uint4 g = gbuf[r];
+			if (IN_COMPACT) {
+				// split by limb into the planes
+				const int u = tid + r * NT;
+				const int q = u / (8 * L), j = u % (8 * L);
+				const uint32_t w[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+				for (int t = 0; t < 4; t++) {
+					const int word = 4 * j + t;
+					lds[(word % L) * kPlane + q * kLimbStride + word / L] = w[t];
+				}
 			} else {
-				mul_tw(ps.field[j], V, W, Pr);  // sub-field circuits reuse W: Pr must not alias it
-			}
-#pragma unroll
-			for (int i = 0; i < 32; i += 4) {
-				uint4 u = *(const uint4*)(pu + i);
-				u.x ^= Pr[i];
-				u.y ^= Pr[i + 1];
-				u.z ^= Pr[i + 2];
-				u.w ^= Pr[i + 3];
-				*(uint4*)(pu + i) = u;
-				*(uint4*)(pv + i) = make_uint4(V[i] ^ u.x, V[i + 1] ^ u.y, V[i + 2] ^ u.z, V[i + 3] ^ u.w);
+				const int u = lane + r * 64;
+				const int q = u >> 3, j = u & 7;
+				*(uint4*)(plane + q * kLimbStride + 4 * j) = g;
 			}
 		}
-	};
-	const int jlow = max(LAST ? 5 : 0, ps.stop_j);
-	for (int j = ps.k - 1; j >= jlow; j--) {
-		if (!(P.dbg & 32)) block_stage(j, tid / L);
-		if (!(P.dbg & 8)) __syncthreads();
-	}
+		const size_t next = tile + gridDim.x;
+		const bool has_next = PF && next < P.ntiles;  // without PF: one tile per workgroup
+		size_t n_outer_v = outer, n_ooff = outer_off;
+		int n_coset = coset;
+		uint32_t* n_dst = dst;
+		const uint32_t* n_src = src;
+		if (has_next) {
+			geo(next, n_outer_v, n_ooff, n_coset, n_dst, n_src);
+			issue(n_src, n_ooff);  // in flight during this tile's stages
+		}
+		if (IN_COMPACT) {
+			// per-(block, limb) 32x32 transposes of this wave's plane
+			__syncthreads();
+			for (int q = lane; q < kTileBlocks; q += 64) {
+				uint32_t* x = plane + q * kLimbStride;
+				uint32_t r[32];
+#pragma unroll
+				for (int i = 0; i < 32; i += 4) *(uint4*)(r + i) = *(const uint4*)(x + i);
+				transpose32(r);
+#pragma unroll
+				for (int i = 0; i < 32; i += 4) *(uint4*)(x + i) = *(const uint4*)(r + i);
+			}
+		}
+		wave_lds_sync();
+		unsigned long long t1 = 0;
+		if (TR) {
+			t1 = ts();
+			tr[0] += t1 - t0;
+		}
 
-	if (LAST) {
-		// ---- stages 4..0 (index bits inside the word), thread-private: thread (pair, limb)
-		// owns blocks qa = pair and qb = pair + 64 for all of them, so no barriers. Per stage
-		// both blocks share one multiply: A's v-lanes move down onto the u positions, B's
-		// v-lanes stay on the v positions (a pair's twiddle depends only on index bits above s).
-		const int qa = tid / L, qb = qa | (kTileBlocks / 2);
-		uint32_t* pa = lds + qa * BLK_WORDS + l * kLimbStride;
-		uint32_t* pb = lds + qb * BLK_WORDS + l * kLimbStride;
-		for (int s = 4; s >= ((P.dbg & 16) ? 5 : ps.stop_j); s--) {  // bottom pass starts at stage 0: j == s
-			{
+		const int jlow = max(LAST ? 5 : 0, ps.stop_j);
+		for (int j = ps.k - 1; j >= jlow; j--) {
+			if (!(P.dbg & 32)) block_stage(j, lane);
+			if (P.dbg & 64)
+				asm volatile("" ::: "memory");  // experiment: rely on in-order LDS execution only
+			else
+				wave_lds_sync();
+		}
+		if (TR) {
+			const unsigned long long t = ts();
+			tr[1] += t - t1;
+			t1 = t;
+		}
+
+		if (LAST) {
+			// ---- stages 4..0 (index bits inside the word), lane-private: lane owns blocks qa = lane
+			// and qb = lane + 64 for all of them. Per stage both blocks share one multiply: A's
+			// v-lanes move down onto the u positions, B's v-lanes stay on the v positions (a pair's
+			// twiddle depends only on index bits above s).
+			const int qa = lane, qb = qa | (kTileBlocks / 2);
+			uint32_t* pa = plane + qa * kLimbStride;
+			uint32_t* pb = plane + qb * kLimbStride;
+			for (int s = 4; s >= ((P.dbg & 16) ? 5 : ps.stop_j); s--) {  // bottom pass starts at stage 0: j == s
 				const int d = 1 << s;
-				const uint32_t um = ~lane_mask(s);
-				const uint32_t ca = cu_lds[s] ^ tile_tw(s, qa), cb = cu_lds[s] ^ tile_tw(s, qb);
+				const uint32_t um = ~lane_mask(s);  // u-lanes (bit s clear)
+				const uint32_t ca = cu_w[s] ^ tile_tw(s, qa), cb = cu_w[s] ^ tile_tw(s, qb);
 				uint32_t W[32], T[32];
 #pragma unroll
 				for (int i = 0; i < 32; i += 4) {
 					const uint4 a = *(const uint4*)(pa + i), b = *(const uint4*)(pb + i);
-					T[i] = ((a.x >> d) & um) | (b.x & ~um);
-					T[i + 1] = ((a.y >> d) & um) | (b.y & ~um);
-					T[i + 2] = ((a.z >> d) & um) | (b.z & ~um);
-					T[i + 3] = ((a.w >> d) & um) | (b.w & ~um);
+					T[i] = __builtin_amdgcn_bitop3_b32(a.x >> d, b.x, um, 0xe4);  // (a>>d & um) | (b & ~um)
+					T[i + 1] = __builtin_amdgcn_bitop3_b32(a.y >> d, b.y, um, 0xe4);
+					T[i + 2] = __builtin_amdgcn_bitop3_b32(a.z >> d, b.z, um, 0xe4);
+					T[i + 3] = __builtin_amdgcn_bitop3_b32(a.w >> d, b.w, um, 0xe4);
 				}
 #pragma unroll
 				for (int i = 0; i < 32; i++)
-					W[i] = ps.pat[s][i] ^ ((0u - ((ca >> i) & 1u)) & um) ^ ((0u - ((cb >> i) & 1u)) & ~um);
+					W[i] = ps.pat[s][i] ^ __builtin_amdgcn_bitop3_b32((uint32_t)__builtin_amdgcn_sbfe(ca, i, 1),
+					                                                  (uint32_t)__builtin_amdgcn_sbfe(cb, i, 1), um, 0xe4);
 				if (P.dbg & 4) {
 #pragma unroll
 					for (int i = 0; i < 32; i++) T[i] ^= W[i];
 				} else {
-					mul_tw(ps.field[s], T, W, T);
+					__builtin_amdgcn_sched_barrier(0);
+					mul_tw<FMAX>(ps.field[s], T, W, T);
+					__builtin_amdgcn_sched_barrier(0);
 				}
 #pragma unroll
 				for (int i = 0; i < 32; i += 4) {
@@ -294,48 +365,72 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 					*(uint4*)Bv = *(const uint4*)(pb + i);
 #pragma unroll
 					for (int t = 0; t < 4; t++) {
-						A[t] ^= T[i + t] & um;
-						Bv[t] ^= (T[i + t] & ~um) >> d;
-						A[t] ^= (A[t] & um) << d;
-						Bv[t] ^= (Bv[t] & um) << d;
+						// u ^= w*v on the u-lanes, then v ^= u: (x & um) << d == (x << d) & ~um and
+						// (x & ~um) >> d == (x >> d) & um for these lane masks
+						const uint32_t a = __builtin_amdgcn_bitop3_b32(T[i + t], um, A[t], 0x6a);         // A ^ (T & um)
+						const uint32_t b = __builtin_amdgcn_bitop3_b32(T[i + t] >> d, um, Bv[t], 0x6a);  // B ^ ((T >> d) & um)
+						A[t] = __builtin_amdgcn_bitop3_b32(a << d, um, a, 0x9a);                          // a ^ ((a << d) & ~um)
+						Bv[t] = __builtin_amdgcn_bitop3_b32(b << d, um, b, 0x9a);
 					}
 					*(uint4*)(pa + i) = *(const uint4*)A;
 					*(uint4*)(pb + i) = *(const uint4*)Bv;
 				}
 			}
-		}
-		// back to compact (limb-split) words, still thread-private
+			// back to compact words (lane-private)
 #pragma unroll
-		for (int h = 0; h < 2; h++) {
-			uint32_t* x = h ? pb : pa;
-			uint32_t r[32];
+			for (int h = 0; h < 2; h++) {
+				uint32_t* x = h ? pb : pa;
+				uint32_t r[32];
 #pragma unroll
-			for (int i = 0; i < 32; i += 4) *(uint4*)(r + i) = *(const uint4*)(x + i);
-			transpose32(r);
+				for (int i = 0; i < 32; i += 4) *(uint4*)(r + i) = *(const uint4*)(x + i);
+				transpose32(r);
 #pragma unroll
-			for (int i = 0; i < 32; i += 4) *(uint4*)(x + i) = *(const uint4*)(r + i);
-		}
-	}
-	__syncthreads();
-
-	// ---- store tile
-	for (int u = tid; u < kTileBlocks * 8 * L; u += NT) {
-		const int q = u / (8 * L), j = u % (8 * L);
-		const uint32_t* b = lds + q * BLK_WORDS;
-		uint4 g;
-		if (LAST) {
-			uint32_t w[4];
-#pragma unroll
-			for (int t = 0; t < 4; t++) {
-				const int word = 4 * j + t;
-				w[t] = b[(word % L) * kLimbStride + word / L];
+				for (int i = 0; i < 32; i += 4) *(uint4*)(x + i) = *(const uint4*)(r + i);
 			}
-			g = make_uint4(w[0], w[1], w[2], w[3]);
-		} else {
-			const int li = (4 * j) / 32, i = (4 * j) % 32;
-			g = *(const uint4*)(b + li * kLimbStride + i);
+			if (TR) {
+				const unsigned long long t = ts();
+				tr[2] += t - t1;
+				t1 = t;
+			}
 		}
-		if (!(P.dbg & 2)) st_stream(dst + (outer_off | tile_off(q)) * L + 4 * j, g);
+
+		// ---- store tile
+		if (LAST) {
+			__syncthreads();  // compact elements gather one word from every limb plane
+			for (int u = tid; u < kTileBlocks * 8 * L; u += NT) {
+				const int q = u / (8 * L), j = u % (8 * L);
+				uint32_t w[4];
+#pragma unroll
+				for (int t = 0; t < 4; t++) {
+					const int word = 4 * j + t;
+					w[t] = lds[(word % L) * kPlane + q * kLimbStride + word / L];
+				}
+				if (!(P.dbg & 2)) st_stream(dst + (outer_off | tile_off(q)) * L + 4 * j, make_uint4(w[0], w[1], w[2], w[3]));
+			}
+		} else {
+#pragma unroll 4
+			for (int r = 0; r < kTileBlocks * 8 / 64; r++) {
+				const int u = lane + r * 64;
+				const int q = u >> 3, j = u & 7;
+				const uint4 g = *(const uint4*)(plane + q * kLimbStride + 4 * j);
+				if (!(P.dbg & 2)) st_stream(dst + (outer_off | tile_off(q)) * L + 32 * l + 4 * j, g);
+			}
+		}
+		if (TR) {
+			tr[3] += ts() - t1;
+			tr[4] += 1;
+		}
+		if (!PF || !has_next) break;
+		tile = next;
+		outer = n_outer_v;
+		outer_off = n_ooff;
+		coset = n_coset;
+		dst = n_dst;
+		src = n_src;
+	}
+	if (TR && lane == 0) {
+		unsigned long long* o = P.trace + ((size_t)blockIdx.x * (NT / 64) + (tid >> 6)) * 8;
+		for (int i = 0; i < 8; i++) o[i] = tr[i];
 	}
 }
 
@@ -410,28 +505,45 @@ static std::vector<BsPass> plan_passes(const bn_antt_plan* plan) {
 	return passes;
 }
 
-template <int L>
-static const void* kernel_for(int role) {
+// kernel instance per (limbs, role, largest stage field); passes whose stages all use GF(2^8)
+// twiddles have registers to spare for prefetching the next tile
+template <int L, int FMAX>
+static const void* kernel_for_f(int role, bool pf) {
 	switch (role) {
-		case ROLE_FIRST: return (const void*)antt_bs_pass<L, ROLE_FIRST>;
-		case ROLE_MID: return (const void*)antt_bs_pass<L, ROLE_MID>;
-		case ROLE_LAST: return (const void*)antt_bs_pass<L, ROLE_LAST>;
-		default: return (const void*)antt_bs_pass<L, ROLE_SINGLE>;
+		case ROLE_FIRST: return pf ? (const void*)antt_bs_pass<L, ROLE_FIRST, FMAX, true> : (const void*)antt_bs_pass<L, ROLE_FIRST, FMAX, false>;
+		case ROLE_MID: return pf ? (const void*)antt_bs_pass<L, ROLE_MID, FMAX, true> : (const void*)antt_bs_pass<L, ROLE_MID, FMAX, false>;
+		case ROLE_LAST: return pf ? (const void*)antt_bs_pass<L, ROLE_LAST, FMAX, true> : (const void*)antt_bs_pass<L, ROLE_LAST, FMAX, false>;
+		default: return pf ? (const void*)antt_bs_pass<L, ROLE_SINGLE, FMAX, true> : (const void*)antt_bs_pass<L, ROLE_SINGLE, FMAX, false>;
 	}
 }
+static const void* kernel_for(int L, int role, int fmax, bool pf) {
+	if (L == 4) return fmax <= 8 ? kernel_for_f<4, 8>(role, pf) : kernel_for_f<4, 32>(role, pf);
+	return fmax <= 8 ? kernel_for_f<1, 8>(role, pf) : kernel_for_f<1, 32>(role, pf);
+}
 
-// tile + one word per stage for the workgroup-uniform twiddle parts
-static size_t lds_bytes(int L) { return ((size_t)kTileBlocks * L * kLimbStride + kMaxStages) * sizeof(uint32_t); }
+static int pass_fmax(const BsPass& p) {
+	int f = 8;
+	for (int j = 0; j < p.k; j++) f = std::max(f, p.field[j]);
+	return f;
+}
+
+// tile + one word per stage and wave for the workgroup-uniform twiddle parts
+static size_t lds_bytes(int L) { return ((size_t)L * kPlane + (size_t)L * kMaxStages) * sizeof(uint32_t); }
 
 bool bs_supports(const bn_antt_plan* plan) {
 	return plan->log_h >= kMinLogH && plan->log_h - 5 - kBlkBits <= kMaxOuter && plan->log_rate <= kMaxRateBits;
 }
 
 int bs_prepare(bn_antt_plan* plan) {
-	for (int role = 0; role < 4; role++) {
-		BN_HIP(hipFuncSetAttribute(kernel_for<4>(role), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(4)));
-		BN_HIP(hipFuncSetAttribute(kernel_for<1>(role), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(1)));
-	}
+	for (int L : {1, 4})
+		for (int role = 0; role < 4; role++)
+			for (int f : {8, 32})
+				for (int pf = 0; pf < 2; pf++)
+					BN_HIP(hipFuncSetAttribute(kernel_for(L, role, f, pf != 0), hipFuncAttributeMaxDynamicSharedMemorySize,
+					                           (int)lds_bytes(L)));
+	int cus = 0;
+	BN_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, plan->device));
+	plan->num_cus = std::max(cus, 1);
 	plan->variant = 1;
 	return BN_OK;
 }
@@ -439,10 +551,15 @@ int bs_prepare(bn_antt_plan* plan) {
 int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st) {
 	const auto passes = plan_passes(plan);
 	const int L = plan->limbs;
-	// debug hooks: BN_DEBUG_MAX_PASSES=n runs only the first n passes,
-	// BN_DEBUG_STOP_STAGE=s runs only stages >= s
+	// debug hooks: BN_DEBUG_MAX_PASSES=n runs only the first n passes, BN_DEBUG_STOP_STAGE=s runs
+	// only stages >= s, BN_PF=1/2 enables next-tile prefetch for GF(2^8)-only / all passes, BN_PERSIST=0 launches
+	// one workgroup per tile, BN_TRACE=1 prints per-wave phase times (cycles)
 	size_t npass = passes.size();
 	if (const char* e = getenv("BN_DEBUG_MAX_PASSES")) npass = std::min(npass, (size_t)atoi(e));
+	int pf_mode = 0;
+	if (const char* e = getenv("BN_PF")) pf_mode = atoi(e);
+	bool persist = true;
+	if (const char* e = getenv("BN_PERSIST")) persist = atoi(e) != 0;
 	for (size_t i = 0; i < npass; i++) {
 		BsParams prm;
 		prm.src = d_in;
@@ -455,14 +572,39 @@ int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t 
 		prm.p.stop_j = 0;
 		if (const char* e = getenv("BN_DEBUG_STOP_STAGE"))
 			prm.p.stop_j = std::max(0, std::min(prm.p.k, atoi(e) - prm.p.lo));
-		const size_t grid = (batch << plan->log_rate) << passes[i].n_outer;
+		const size_t ntiles = (batch << plan->log_rate) << passes[i].n_outer;
+		// two 74-KB tiles per CU: a persistent grid of two workgroups per CU walks all tiles
+		const int fmax = pass_fmax(passes[i]);
+		const bool pf = persist && (pf_mode == 2 || (pf_mode == 1 && fmax <= 8));
+		const size_t grid = pf ? std::min(ntiles, (size_t)2 * (size_t)plan->num_cus) : ntiles;
+		prm.ntiles = ntiles;
+		prm.trace = nullptr;
+		static unsigned long long* trbuf = nullptr;
+		if (getenv("BN_TRACE")) {
+			if (!trbuf) BN_HIP(hipMalloc(&trbuf, (size_t)1 << 26));
+			BN_HIP(hipMemset(trbuf, 0, grid * L * 8 * 8));
+			prm.trace = trbuf;
+		}
 		int rc = timing_begin(plan, (int)i, st);
 		if (rc != BN_OK) return rc;
 		void* args[] = {&prm};
-		const void* fn = L == 4 ? kernel_for<4>(passes[i].role) : kernel_for<1>(passes[i].role);
-		BN_HIP(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(64 * L), args, lds_bytes(L), st));
+		BN_HIP(hipLaunchKernel(kernel_for(L, passes[i].role, fmax, pf), dim3((unsigned)grid), dim3(64 * L), args,
+		                       lds_bytes(L), st));
 		rc = timing_end(plan, (int)i, st);
 		if (rc != BN_OK) return rc;
+		if (prm.trace) {
+			const size_t g = grid * (size_t)L;
+			std::vector<unsigned long long> h(g * 8);
+			BN_HIP(hipStreamSynchronize(st));
+			BN_HIP(hipMemcpy(h.data(), prm.trace, g * 8 * 8, hipMemcpyDeviceToHost));
+			double acc[8] = {0};
+			for (size_t w = 0; w < g; w++)
+				for (int k = 0; k < 8; k++) acc[k] += (double)h[w * 8 + k];
+			const double t = acc[4] > 0 ? acc[4] : 1;  // wave-tiles
+			fprintf(stderr,
+			        "trace pass %zu (fmax %d pf %d, %zu wave-tiles, cycles per wave-tile): load %.0f  block %.0f [pre %.0f mul %.0f post %.0f]  inword+tr %.0f  store %.0f\n",
+			        i, fmax, (int)pf, (size_t)acc[4], acc[0] / t, acc[1] / t, acc[5] / t, acc[6] / t, acc[7] / t, acc[2] / t, acc[3] / t);
+		}
 	}
 	return BN_OK;
 }

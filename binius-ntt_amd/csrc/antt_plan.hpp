@@ -16,6 +16,7 @@ struct bn_antt_plan {
 	int limbs = 4;   // u32 words per element
 	int width = 0;   // log_h + log_rate - 1 (columns of the subspace table)
 	int variant = 0; // kernel path in use (see antt.hip)
+	int num_cus = 0; // compute units of the device (persistent grids)
 	std::vector<uint32_t> s_host;  // log_h x width, row-major
 	uint32_t* s_dev = nullptr;     // same on the device
 	uint32_t* scratch = nullptr;   // pass-intermediate buffer (variant-specific)

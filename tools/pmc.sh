@@ -16,5 +16,6 @@ run() {  # name, counters...
 run fetch FETCH_SIZE && run write WRITE_SIZE \
  && run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU \
  && run lds SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE \
+ && run stall SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT \
  && run ic SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY \
  && echo pmc done
