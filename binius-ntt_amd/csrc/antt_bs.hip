@@ -336,7 +336,7 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 			for (int s = 4; s >= ((P.dbg & 16) ? 5 : ps.stop_j); s--) {  // bottom pass starts at stage 0: j == s
 				const int d = 1 << s;
 				const uint32_t um = ~lane_mask(s);  // u-lanes (bit s clear)
-				const uint32_t ca = cu_w[s] ^ tile_tw(s, qa), cb = cu_w[s] ^ tile_tw(s, qb);
+				const uint32_t cb = cu_w[s] ^ tile_tw(s, qb);
 				uint32_t W[32], T[32];
 #pragma unroll
 				for (int i = 0; i < 32; i += 4) {
@@ -346,10 +346,10 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 					T[i + 2] = __builtin_amdgcn_bitop3_b32(a.z >> d, b.z, um, 0xe4);
 					T[i + 3] = __builtin_amdgcn_bitop3_b32(a.w >> d, b.w, um, 0xe4);
 				}
+				// twiddle word i: pattern (bit-lane bits s+1..4) ^ block part, cb on B's lanes and
+				// ca = cb ^ twt[s][6] on A's (um) lanes; the host folds the um & twt[s][6] part into pat
 #pragma unroll
-				for (int i = 0; i < 32; i++)
-					W[i] = ps.pat[s][i] ^ __builtin_amdgcn_bitop3_b32((uint32_t)__builtin_amdgcn_sbfe(ca, i, 1),
-					                                                  (uint32_t)__builtin_amdgcn_sbfe(cb, i, 1), um, 0xe4);
+				for (int i = 0; i < 32; i++) W[i] = ps.pat[s][i] ^ (uint32_t)__builtin_amdgcn_sbfe(cb, i, 1);
 				if (P.dbg & 4) {
 #pragma unroll
 					for (int i = 0; i < 32; i++) T[i] ^= W[i];
@@ -481,6 +481,9 @@ static std::vector<BsPass> plan_passes(const bn_antt_plan* plan) {
 					uint32_t w = 0;
 					for (int b = s + 1; b < 5; b++)
 						if ((S(s, b - s - 1) >> i) & 1) w ^= lane_mask(b);
+					// A's v-lanes sit on the u positions with twiddle cb ^ twt[s][6] (qa, qb differ in
+					// tile bit 6 only): fold that uniform difference in
+					if ((p.twt[j][kBlkBits - 1] >> i) & 1) w ^= ~lane_mask(s);
 					p.pat[s][i] = w;
 				}
 			}
