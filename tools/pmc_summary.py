@@ -5,7 +5,7 @@ Per MI355X_MICROARCH.md (HBM section): FETCH_SIZE reports half the bytes of wide
 streaming reads on gfx950 -> doubled here; WRITE_SIZE reads exact for 16-B stores. Both are
 in KiB. Prints the per-kernel mean per dispatch and writes gpurun_out/pmc_summary.json.
 With --traffic LOG_H it also writes profiles/pmc_traffic.json: {LOG_H: HBM bytes per launch of
-the headline NTT's dominant kernel (the bottom pass, antt_bs_pass<4, 2>)}, read by bench.py.
+the headline NTT's dominant kernel (the bottom pass, antt_bs_pass<4, 2, ...>)}, read by bench.py.
 """
 import csv
 import glob
@@ -49,7 +49,7 @@ def main():
     with open(os.path.join(root, "pmc_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
     if traffic_log_h:
-        dom = [k for k in out if "antt_bs_pass<4, 2>" in k]
+        dom = [k for k in out if "antt_bs_pass<4, 2" in k]
         if dom and "HBM_READ_BYTES_corrected" in out[dom[0]] and "HBM_WRITE_BYTES" in out[dom[0]]:
             m = out[dom[0]]
             path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
