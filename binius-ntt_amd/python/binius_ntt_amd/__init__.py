@@ -84,6 +84,10 @@ def lib():
         "bn_multilinear_composition_eval": (i32, [i32, i32, i32, i32, u32p, u32p, u32p]),
         "bn_multilinear_composition_eval_device": (i32, [i32, i32, i32, i32, vp, u32p, u32p]),
         "bn_sumcheck_interpolate": (i32, [u32p, i32, u32p, u32p]),
+        "bn_bb31_ntt_plan_create": (i32, [i32, ctypes.c_uint32, i32, i32, ctypes.POINTER(vp)]),
+        "bn_bb31_ntt_plan_destroy": (i32, [vp]),
+        "bn_bb31_ntt_forward_host": (i32, [vp, vp, sz, vp, i32]),
+        "bn_bb31_ntt_forward_device": (i32, [vp, vp, vp, sz, i32, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -246,6 +250,96 @@ class AdditiveNTT:
         n = ctypes.c_int()
         _check(lib().bn_antt_get_event_timing(self._plan, arr, 16, ctypes.byref(n)))
         return [arr[i] for i in range(min(n.value, 16))]
+
+
+# ------------------------------------------------------------------ BabyBear NTT (prime-field sibling)
+class BB31:
+    """risc0::Fp value (src/ulvt/finite_fields/risc0_baby_bear.h:40-190), canonical int view:
+    BB31(r) == r mod p, asUInt32() returns the canonical value."""
+    P = 15 * (1 << 27) + 1
+
+    def __init__(self, v=0):
+        self.v = int(v) % self.P
+
+    def asUInt32(self):
+        return self.v
+
+    def __mul__(self, o):
+        return BB31(self.v * o.v)
+
+    def __add__(self, o):
+        return BB31(self.v + o.v)
+
+    def __sub__(self, o):
+        return BB31(self.v - o.v)
+
+    def __eq__(self, o):
+        return isinstance(o, BB31) and self.v == o.v
+
+    @staticmethod
+    def pow(x, n):
+        return BB31(pow(x.v, int(n), BB31.P))
+
+    @staticmethod
+    def inv(x):
+        return BB31(pow(x.v, BB31.P - 2, BB31.P))
+
+    @staticmethod
+    def one():
+        return BB31(1)
+
+
+class NTTConfRad2:
+    """nttconf.cuh:25-47; the reference ASSERTs on bad parameters, this raises."""
+
+    def __init__(self, generator, log_group_order, log_inp_size, device=0):
+        if not 1 <= log_inp_size <= 27:
+            raise ValueError("log_inp_size must be in [1, 27]")
+        if not log_group_order >= log_inp_size:
+            raise ValueError("log_group_order must be >= log_inp_size")
+        self.generator = generator if isinstance(generator, BB31) else BB31(generator)
+        self.log_group_order, self.log_inp_size, self.device = log_group_order, log_inp_size, device
+
+
+class NTT:
+    """NTT<BB31> (gpuntt.cuh:126-209) over the C-ABI plan: natural-order DFT with
+    w = generator^(2^(log_group_order - log_inp_size))."""
+
+    def __init__(self, conf):
+        self.conf = conf
+        p = ctypes.c_void_p()
+        _check(lib().bn_bb31_ntt_plan_create(conf.device, conf.generator.v, conf.log_group_order,
+                                             conf.log_inp_size, ctypes.byref(p)))
+        self._plan = p
+
+    def close(self):
+        if getattr(self, "_plan", None) is not None and self._plan.value:
+            lib().bn_bb31_ntt_plan_destroy(self._plan)
+            self._plan = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def apply(self, inp, out):
+        """Reference semantics: input of 2^log_inp_size canonical words, IN_ORDER or
+        BIT_REVERSED; output in order (raises where the reference ASSERTs)."""
+        n = 1 << self.conf.log_inp_size
+        if inp.size != n:
+            raise ValueError("input has %d elements, plan expects %d" % (inp.size, n))
+        src = np.ascontiguousarray(inp.data, dtype=np.uint32)
+        if out.data.size != n:
+            out.data = np.zeros(n, np.uint32)
+            out.size = n
+        br = 1 if inp.order == DataOrder.BIT_REVERSED else 0
+        _check(lib().bn_bb31_ntt_forward_host(self._plan, src.ctypes.data, n, out.data.ctypes.data, br))
+        out.order = DataOrder.IN_ORDER
+
+    def forward_device(self, d_in, d_out, batch=1, bit_reversed=False, stream=None):
+        _check(lib().bn_bb31_ntt_forward_device(self._plan, _ptr(d_in), _ptr(d_out), batch,
+                                                1 if bit_reversed else 0, _stream(stream)))
 
 
 # ------------------------------------------------------------------ field / bitslicing

@@ -171,6 +171,34 @@ int bn_multilinear_composition_eval_device(int device, int num_vars, int composi
  * at `challenge`. Host arithmetic; 1 <= num_points <= 16. */
 int bn_sumcheck_interpolate(const uint32_t* points, int num_points, const uint32_t* challenge, uint32_t* out);
 
+
+/* ------------------------------------------------------------------------------------
+ * BabyBear radix-2 NTT, the prime-field sibling path (src/ulvt/ntt/gpuntt.cuh,
+ * NTTConfRad2 in src/ulvt/ntt/nttconf.cuh:25-47, BB31 = risc0::Fp,
+ * src/ulvt/finite_fields/risc0_baby_bear.h:40-190). Elements are uint32_t holding the
+ * canonical value (BB31::asUInt32(); inputs are reduced mod p = 15*2^27+1 as BB31(r) does).
+ * The transform is the natural-order DFT X[k] = sum_j x[j] w^(jk), w = g^(2^(log_group-log_n)).
+ * ------------------------------------------------------------------------------------ */
+typedef struct bn_bb31_ntt_plan bn_bb31_ntt_plan;
+
+/* Replaces NTTConfRad2<BB31>(generator, log_group_order, log_inp_size) (nttconf.cuh:31-38:
+ * 1 <= log_n <= 27, log_group_order >= log_n) + the NTT<BB31> constructor (gpuntt.cuh:128-146,
+ * twiddle precomputation). generator is a canonical value (BB31(137) -> 137). */
+int bn_bb31_ntt_plan_create(int device, uint32_t generator, int log_group_order, int log_n, bn_bb31_ntt_plan** plan);
+int bn_bb31_ntt_plan_destroy(bn_bb31_ntt_plan* plan);
+
+/* Replaces NTT<BB31>::apply(input, output) (gpuntt.cuh:150-183): host in -> host out,
+ * synchronous, output in order. in_bit_reversed = 1 for NTTData::order == BIT_REVERSED (the
+ * input is used as stored), 0 for IN_ORDER. BN_ERR_INVALID if in_elems != 2^log_n (the
+ * reference ASSERTs). */
+int bn_bb31_ntt_forward_host(bn_bb31_ntt_plan* plan, const uint32_t* in, size_t in_elems, uint32_t* out,
+                             int in_bit_reversed);
+
+/* Device-resident, asynchronous on `stream` (hipStream_t, NULL = default): batch transforms of
+ * 2^log_n words each, contiguous; d_in and d_out must not overlap. */
+int bn_bb31_ntt_forward_device(bn_bb31_ntt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch,
+                               int in_bit_reversed, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -101,6 +101,14 @@ void orc_md5(const void* data, size_t len, uint8_t digest[16]);
 /* MD5 of one limb plane (limb in 0..3) of a 4-word-per-element vector */
 void orc_md5_limb(const uint32_t* v, size_t n_elems, int limb, uint8_t digest[16]);
 
+
+/* ---------------- BabyBear radix-2 NTT (prime-field sibling path, bb31.c) ----------------
+ * Canonical u32 values (< 2013265921); inputs are reduced mod p as BB31(r) does.            */
+uint32_t orc_bb31_mul(uint32_t a, uint32_t b);
+uint32_t orc_bb31_pow(uint32_t x, uint64_t n);
+uint32_t orc_bb31_inv(uint32_t x);
+void     orc_bb31_ntt(const uint32_t* in, uint32_t* out, int log_n, uint32_t gen, int log_group, int in_bit_reversed);
+
 #ifdef __cplusplus
 }
 #endif

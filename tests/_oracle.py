@@ -56,6 +56,14 @@ def lib():
         L.orc_fill128.argtypes = [ctypes.c_uint32, ctypes.c_uint64, _u32p, ctypes.c_size_t]
         L.orc_md5.argtypes = [ctypes.c_void_p, ctypes.c_size_t, _u8p]
         L.orc_md5_limb.argtypes = [_u32p, ctypes.c_size_t, ctypes.c_int, _u8p]
+        L.orc_bb31_mul.restype = ctypes.c_uint32
+        L.orc_bb31_mul.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+        L.orc_bb31_pow.restype = ctypes.c_uint32
+        L.orc_bb31_pow.argtypes = [ctypes.c_uint32, ctypes.c_uint64]
+        L.orc_bb31_inv.restype = ctypes.c_uint32
+        L.orc_bb31_inv.argtypes = [ctypes.c_uint32]
+        L.orc_bb31_ntt.restype = None
+        L.orc_bb31_ntt.argtypes = [_u32p, _u32p, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
         L.orc_init()
         _LIB = L
     return _LIB
@@ -199,4 +207,15 @@ def multilinear_composition(evals_compact, n, d, challenges):
     out = np.zeros(4, np.uint32)
     lib().orc_multilinear_composition(np.ascontiguousarray(evals_compact, dtype=np.uint32).reshape(-1), n, d,
                                       np.ascontiguousarray(challenges, dtype=np.uint32).reshape(-1), out)
+    return out
+
+
+BB31_P = 2013265921
+
+
+def bb31_ntt(x, log_n, gen=137, log_group=27, bit_reversed=False):
+    """BabyBear radix-2 NTT (reference NTT<BB31>::apply semantics, gpuntt.cuh:150-183)."""
+    x = np.ascontiguousarray(x, dtype=np.uint32)
+    out = np.empty(1 << log_n, dtype=np.uint32)
+    lib().orc_bb31_ntt(x, out, log_n, gen, log_group, 1 if bit_reversed else 0)
     return out
