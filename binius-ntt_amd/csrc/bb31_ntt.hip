@@ -148,17 +148,20 @@ __global__ __launch_bounds__(kThreads) void bb_pass(BbArgs A) {
 		if (ROLE == 1) return ((kb * kCols + c) << (A.log_n - ps.m1)) + gpos + r;
 		return ps.bitrev_in ? (size_t)rev_bits((uint32_t)r, A.log_n) : (size_t)r;
 	};
-	// LDS: row r, column c at r * cols + c (a row of 32 words spans half the banks)
+	// LDS: row r, column c at r * cols + c (a row of 32 words spans half the banks); behind the
+	// tile, the tile DFT's twiddles w_R^i (Montgomery-encoded), i < R/2
+	uint32_t* twl = lds + W;
+	for (int i = tid; i < R / 2; i += kThreads) twl[i] = wpow(A, (uint32_t)i << (A.log_n - m));
 	for (int u = tid; u < W; u += kThreads) {
 		const int r = u / cols, c = u % cols;
 		lds[u] = bb_reduce(src[src_addr(r, c)]);
 	}
 	__syncthreads();
-	// radix-2 DIF stages: natural-order rows in, bit-reversed rows out
+	// radix-2 DIF stages: natural-order rows in, bit-reversed rows out; stage st uses
+	// w_{2 half}^k = w_R^(k R / (2 half))
 	const int pairs = (R / 2) * cols;
 	for (int st = m - 1; st >= 0; st--) {
 		const int half = 1 << st;
-		// twiddle w_{2 half}^{k} = w^{k * 2^(log_n - st - 1)}
 		for (int u = tid; u < pairs; u += kThreads) {
 			const int c = u % cols, pr = u / cols;
 			const int k = pr & (half - 1);
@@ -168,23 +171,33 @@ __global__ __launch_bounds__(kThreads) void bb_pass(BbArgs A) {
 			const uint32_t x = *pu, y = *pv;
 			*pu = bb_add(x, y);
 			const uint32_t d = bb_sub(x, y);
-			*pv = k ? mont(d, wpow(A, (uint32_t)k << (A.log_n - st - 1))) : d;
+			*pv = k ? mont(d, twl[k << (m - 1 - st)]) : d;
 		}
 		__syncthreads();
 	}
-	// write row k (held at LDS row rev_m(k)); inter-pass twiddle w_{M_{p-1}}^(c k)
-	for (int u = tid; u < W; u += kThreads) {
-		const int k = u / cols, c = u % cols;
-		uint32_t v = lds[rev_bits((uint32_t)k, m) * cols + c];
-		if (ROLE == 0) {
-			const size_t cf = cb * kCols + c;  // column index inside the sub-problem
-			const size_t e = (cf * (size_t)k) & (((size_t)1 << ps.log_sub) - 1);
-			if (e) v = mont(v, wpow(A, (uint32_t)(e << (A.log_n - ps.log_sub))));
+	// write row k (held at LDS row rev_m(k)). ROLE 0: inter-pass twiddle w_{M_{p-1}}^(c k); a
+	// lane keeps its column c and walks rows k = k0, k0 + 8, ... so the twiddle advances by one
+	// Montgomery product per element from two table lookups per lane.
+	if (ROLE == 0) {
+		const int c = tid % kCols, k0 = tid / kCols;  // kThreads / kCols = 8 rows per sweep
+		const size_t cf = cb * kCols + c;             // column index inside the sub-problem
+		const size_t msk = ((size_t)1 << ps.log_sub) - 1;
+		const int sh = A.log_n - ps.log_sub;
+		uint32_t tw = wpow(A, (uint32_t)(((cf * (size_t)k0) & msk) << sh));
+		const uint32_t step = wpow(A, (uint32_t)(((cf * (size_t)(kThreads / kCols)) & msk) << sh));
+		for (int k = k0; k < R; k += kThreads / kCols) {
+			const uint32_t v = mont(lds[rev_bits((uint32_t)k, m) * kCols + c], tw);
 			dst[(q << ps.log_sub) + ((size_t)k << ps.log_mp) + cf] = v;
-		} else if (ROLE == 1) {
-			dst[(kb * kCols + c) + gout + ((size_t)k << (A.log_n - m))] = v;
-		} else {
-			dst[k] = v;
+			tw = mont(tw, step);
+		}
+	} else {
+		for (int u = tid; u < W; u += kThreads) {
+			const int k = u / cols, c = u % cols;
+			const uint32_t v = lds[rev_bits((uint32_t)k, m) * cols + c];
+			if (ROLE == 1)
+				dst[(kb * kCols + c) + gout + ((size_t)k << (A.log_n - m))] = v;
+			else
+				dst[k] = v;
 		}
 	}
 }
@@ -293,7 +306,7 @@ extern "C" int bn_bb31_ntt_plan_create(int device, uint32_t generator, int log_g
 	if (e == hipSuccess) e = hipMemcpy(P->wtab, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
 	if (e == hipSuccess)
 		for (const void* f : {pass_fn<0>(), pass_fn<1>(), pass_fn<2>()})
-			if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (1 << kMaxM) * kCols * 4);
+			if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, ((1 << kMaxM) * kCols + (1 << 12)) * 4);
 	hipSetDevice(prev);
 	if (e != hipSuccess) {
 		bn_bb31_ntt_plan_destroy(P);
@@ -356,7 +369,8 @@ static int bb_forward(bn_bb31_ntt_plan* P, const uint32_t* d_in, uint32_t* d_out
 		}
 		void* args[] = {&A};
 		const void* fn = p.role == 0 ? pass_fn<0>() : p.role == 1 ? pass_fn<1>() : pass_fn<2>();
-		BN_HIP(hipLaunchKernel(fn, dim3((unsigned)tiles, (unsigned)batch), dim3(kThreads), args, (size_t)W * 4, st));
+		BN_HIP(hipLaunchKernel(fn, dim3((unsigned)tiles, (unsigned)batch), dim3(kThreads), args,
+		                       ((size_t)W + ((size_t)1 << p.m) / 2) * 4, st));
 	}
 	return BN_OK;
 }

@@ -12,6 +12,9 @@ c4  Sumcheck over GF(2^128), 2^N evals, bitsliced input (DATA_IS_TRANSPOSED = tr
 c5  one GPU's share of the 256 x 2^20 batched NTT (32 transforms), elements/s; and one GPU's
     shard (rank 0 of 8) of the 2^28-eval d=3 sumcheck: the sharded rounds up to the endgame
     gather (the per-round all-gather of (d+2)x16 B partials is not included).
+bb  BabyBear radix-2 NTT (prime-field sibling): 2^24 single transform and
+    16 x 2^20 batched, device-resident, elements/s and algorithmic GB/s (4 B read + 4 B written
+    per element).
 Every line is one JSON object.
 """
 import argparse
@@ -147,9 +150,24 @@ def c5_sumcheck_shard(dev, out, nvars=28, d=3, world=8):
          % (nvars, d, world, r), "value": (1 << nvars) / world / dt, "unit": "evals/s (this shard)", "ms": dt * 1e3})
 
 
+def bb_line(dev, out, log_n, batch):
+    import torch
+    import binius_ntt_amd as B
+    st = torch.cuda.current_stream(dev)
+    n = 1 << log_n
+    x = torch.from_numpy(np.random.default_rng(9).integers(0, 2**32, size=n * batch, dtype=np.uint64)
+                         .astype(np.uint32).view(np.int32)).to(dev)
+    y = torch.empty_like(x)
+    ntt = B.NTT(B.NTTConfRad2(B.BB31(137), 27, log_n))
+    ms = ev_time(lambda: ntt.forward_device(x, y, batch=batch, stream=st), 20, st)
+    out({"config": "bb", "workload": "BabyBear NTT 2^%d x %d (natural order in/out)" % (log_n, batch),
+         "value": n * batch / (ms * 1e-3), "unit": "elements/s", "ms": ms,
+         "hbm_gbps_algorithmic": 8 * n * batch / (ms * 1e-3) / 1e9})
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="c2,c3,c4,c5")
+    ap.add_argument("--only", default="c2,c3,c4,c5,bb")
     ap.add_argument("--sc-vars", type=int, default=24)
     ap.add_argument("--sc-d", default="2,3,4")
     ap.add_argument("--out", default=None)
@@ -173,6 +191,9 @@ def main():
         ntt_line(dev, out, "c5 (per-GPU share)", 20, 32)
         c5_sumcheck_shard(dev, out)
         c5_sumcheck_single(dev, out)
+    if "bb" in only:
+        bb_line(dev, out, 24, 1)
+        bb_line(dev, out, 20, 16)
     if a.out:
         with open(a.out, "w") as f:
             for d in lines:
