@@ -88,6 +88,11 @@ def lib():
         "bn_bb31_ntt_plan_destroy": (i32, [vp]),
         "bn_bb31_ntt_forward_host": (i32, [vp, vp, sz, vp, i32]),
         "bn_bb31_ntt_forward_device": (i32, [vp, vp, vp, sz, i32, vp]),
+        "bn_qm31_sumcheck_create": (i32, [i32, i32, u32p, ctypes.POINTER(vp)]),
+        "bn_qm31_sumcheck_round_messages": (i32, [vp, u32p]),
+        "bn_qm31_sumcheck_fold": (i32, [vp, u32p]),
+        "bn_qm31_sumcheck_final_values": (i32, [vp, u32p]),
+        "bn_qm31_sumcheck_destroy": (i32, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -199,6 +199,27 @@ int bn_bb31_ntt_forward_host(bn_bb31_ntt_plan* plan, const uint32_t* in, size_t 
 int bn_bb31_ntt_forward_device(bn_bb31_ntt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch,
                                int in_bit_reversed, void* stream);
 
+
+/* ------------------------------------------------------------------------------------
+ * QM31 sumcheck, the prime-field sibling of the GF(2^128) sumcheck
+ * (src/ulvt/prime_field_sumcheck/sumcheck.cuh:8-96, core/kernels.cu:5-77). A QM31 element
+ * is 4 uint32_t M31 words (lo.a, lo.b, hi.a, hi.b), canonical (< 2^31 - 1) on output.
+ * ------------------------------------------------------------------------------------ */
+typedef struct bn_qm31_sumcheck bn_qm31_sumcheck;
+
+/* Replaces Sumcheck<NUM_VARS>(evals, benchmarking) (sumcheck.cuh:24-44): evals = column 0 then
+ * column 1, 2^num_vars QM31 each (8 * 2^num_vars words); 1 <= num_vars <= 28 (the reference
+ * instantiates 1, 20, 24, 28). */
+int bn_qm31_sumcheck_create(int device, int num_vars, const uint32_t* evals, bn_qm31_sumcheck** sc);
+/* Replaces this_round_messages<BLOCKS, THREADS>(points) (sumcheck.cuh:46-86): points 0, 1, 2
+ * (12 words). */
+int bn_qm31_sumcheck_round_messages(bn_qm31_sumcheck* sc, uint32_t* points);
+/* Replaces fold<BLOCKS, THREADS>(challenge) (sumcheck.cuh:88-96). */
+int bn_qm31_sumcheck_fold(bn_qm31_sumcheck* sc, const uint32_t* challenge);
+/* After the last fold: the two remaining values f0(r), f1(r) (8 words). */
+int bn_qm31_sumcheck_final_values(bn_qm31_sumcheck* sc, uint32_t* out);
+int bn_qm31_sumcheck_destroy(bn_qm31_sumcheck* sc);
+
 #ifdef __cplusplus
 }
 #endif

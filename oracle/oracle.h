@@ -109,6 +109,13 @@ uint32_t orc_bb31_pow(uint32_t x, uint64_t n);
 uint32_t orc_bb31_inv(uint32_t x);
 void     orc_bb31_ntt(const uint32_t* in, uint32_t* out, int log_n, uint32_t gen, int log_group, int in_bit_reversed);
 
+
+/* ---------------- QM31 sumcheck (prime-field sibling path, qm31.c) ----------------
+ * QM31 element = 4 canonical M31 words (lo.a, lo.b, hi.a, hi.b) as qm31.cuh's member order.  */
+void orc_qm31_mul(const uint32_t* a, const uint32_t* b, uint32_t* out);
+void orc_qm31_interpolate(const uint32_t* points, const uint32_t* r, uint32_t* out);
+void orc_qm31_sumcheck_run(uint32_t* evals, int n, const uint32_t* challenges, uint32_t* points);
+
 #ifdef __cplusplus
 }
 #endif

@@ -64,6 +64,12 @@ def lib():
         L.orc_bb31_inv.argtypes = [ctypes.c_uint32]
         L.orc_bb31_ntt.restype = None
         L.orc_bb31_ntt.argtypes = [_u32p, _u32p, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
+        L.orc_qm31_mul.restype = None
+        L.orc_qm31_mul.argtypes = [_u32p, _u32p, _u32p]
+        L.orc_qm31_interpolate.restype = None
+        L.orc_qm31_interpolate.argtypes = [_u32p, _u32p, _u32p]
+        L.orc_qm31_sumcheck_run.restype = None
+        L.orc_qm31_sumcheck_run.argtypes = [_u32p, ctypes.c_int, _u32p, _u32p]
         L.orc_init()
         _LIB = L
     return _LIB
@@ -219,3 +225,32 @@ def bb31_ntt(x, log_n, gen=137, log_group=27, bit_reversed=False):
     out = np.empty(1 << log_n, dtype=np.uint32)
     lib().orc_bb31_ntt(x, out, log_n, gen, log_group, 1 if bit_reversed else 0)
     return out
+
+
+M31_P = (1 << 31) - 1
+
+
+def qm31(x):
+    """QM31 value as 4 canonical words (lo.a, lo.b, hi.a, hi.b)."""
+    return np.array([v % M31_P for v in x], dtype=np.uint32)
+
+
+def qm31_mul(a, b):
+    out = np.zeros(4, np.uint32)
+    lib().orc_qm31_mul(qm31(a), qm31(b), out)
+    return out
+
+
+def qm31_interpolate(points, r):
+    out = np.zeros(4, np.uint32)
+    lib().orc_qm31_interpolate(np.ascontiguousarray(points, dtype=np.uint32).reshape(-1), qm31(r), out)
+    return out
+
+
+def qm31_sumcheck_run(evals, n, challenges):
+    """evals: (2, 2^n, 4) uint32 (copied); challenges: (n, 4). Returns points (n, 3, 4)."""
+    e = np.ascontiguousarray(evals, dtype=np.uint32).reshape(-1).copy()
+    ch = np.ascontiguousarray(challenges, dtype=np.uint32).reshape(-1)
+    pts = np.zeros(12 * n, np.uint32)
+    lib().orc_qm31_sumcheck_run(e, n, ch, pts)
+    return pts.reshape(n, 3, 4)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Secondary benchmark lines for BASELINE.json configs 2-5 (bench.py keeps the headline NTT).
 
-  python tools/bench_configs.py [--only c2,c3,c4,c5] [--sc-vars 24] [--out FILE]
+  python tools/bench_configs.py [--only c2,c3,c4,c5,bb,qm] [--sc-vars 24] [--out FILE]
 
 c2  GF(2^128) multiply microbench, register-resident repeat loops (bitsliced_repeat style):
     compact (one element per lane) and bitsliced (32 products per lane-block), products/s.
@@ -15,6 +15,10 @@ c5  one GPU's share of the 256 x 2^20 batched NTT (32 transforms), elements/s; a
 bb  BabyBear radix-2 NTT (prime-field sibling): 2^24 single transform and
     16 x 2^20 batched, device-resident, elements/s and algorithmic GB/s (4 B read + 4 B written
     per element).
+qm  QM31 sumcheck (prime-field sibling), two columns of 2^N QM31, product
+    composition: all N rounds (round messages + fold, one host round trip per round as in
+    sumcheck.cuh:46-96) on device-resident columns; evals/s = 2^N / t (wall clock, setup upload
+    excluded as the reference's benchmarking timer does).
 Every line is one JSON object.
 """
 import argparse
@@ -165,9 +169,33 @@ def bb_line(dev, out, log_n, batch):
          "hbm_gbps_algorithmic": 8 * n * batch / (ms * 1e-3) / 1e9})
 
 
+def qm_line(dev, out, nvars, reps=3):
+    import torch
+    import binius_ntt_amd.prime_field as PF
+    ev = np.random.default_rng(11).integers(0, 2**31 - 1, size=(2 << nvars, 4), dtype=np.uint64).astype(np.uint32)
+    r = PF.QM31([32482843, 85864538, 8348234, 9544334])
+    best = None
+    for _ in range(reps):
+        sc = PF.Sumcheck(nvars, ev, device=dev.index or 0)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(nvars):
+            sc.this_round_messages()
+            sc.fold(r)
+        sc.final_values()
+        dt = time.perf_counter() - t0
+        sc.close()
+        best = dt if best is None else min(best, dt)
+    out({"config": "qm", "workload": "QM31 sumcheck 2 x 2^%d, d=2, all rounds" % nvars,
+         "value": (1 << nvars) / best, "unit": "evals/s", "ms": best * 1e3,
+         # per round over cur pairs: messages read 2 x 16 B x cur, fold reads the same and writes
+         # half; sum of cur over rounds ~ 2 x 2^N  ->  160 B per eval
+         "hbm_gbps_algorithmic": 160 * (1 << nvars) / best / 1e9})
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="c2,c3,c4,c5,bb")
+    ap.add_argument("--only", default="c2,c3,c4,c5,bb,qm")
     ap.add_argument("--sc-vars", type=int, default=24)
     ap.add_argument("--sc-d", default="2,3,4")
     ap.add_argument("--out", default=None)
@@ -194,6 +222,8 @@ def main():
     if "bb" in only:
         bb_line(dev, out, 24, 1)
         bb_line(dev, out, 20, 16)
+    if "qm" in only:
+        qm_line(dev, out, 24)
     if a.out:
         with open(a.out, "w") as f:
             for d in lines:
