@@ -11,10 +11,12 @@
 // copies per round); a round's messages are one streaming pass with 16-byte loads of the four
 // rows a lane needs, the per-component sums are exact 64-bit integers (as sum_into_u64) reduced
 // through wave shuffles and LDS, one 64-bit atomic per workgroup and value, and read back through
-// pinned memory; the fold is a second streaming pass. Values are canonical (< p) throughout.
+// pinned memory. fold(r) is deferred and fused into the next round's messages pass, so each
+// round streams the columns once. Values are canonical (< p) throughout.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 
@@ -28,6 +30,9 @@ struct bn_qm31_sumcheck {
 	unsigned long long* h_acc = nullptr;  // pinned
 	hipStream_t stream = nullptr;
 	int cus = 256;
+	int wg_per_cu = 8;  // grid cap (BN_QM_WG_PER_CU overrides, for tuning)
+	bool pending = false;  // a fold(r) not yet applied to cols (fused into the next round's messages)
+	uint4 pend_r = {0, 0, 0, 0};
 };
 
 namespace bn {
@@ -87,25 +92,19 @@ __global__ __launch_bounds__(kT) void qm_reduce(uint32_t* w, size_t n) {
 	for (size_t i = (size_t)blockIdx.x * kT + threadIdx.x; i < n; i += (size_t)gridDim.x * kT) w[i] = m_red(w[i]);
 }
 
-// round messages: lanes stride over x < h; exact u64 component sums -> one atomic per value per WG
-__global__ __launch_bounds__(kT) void qm_messages(const uint32_t* cols, size_t col_words, size_t h,
-                                                  unsigned long long* acc) {
-	unsigned long long s[12];
+__device__ inline void qm_accumulate(unsigned long long (&s)[12], Qm l0, Qm u0, Qm l1, Qm u1) {
+	const Qm p[3] = {q_mul(l0, l1), q_mul(u0, u1), q_mul(q_add(q_sub(u0, l0), u0), q_add(q_sub(u1, l1), u1))};
 #pragma unroll
-	for (int i = 0; i < 12; i++) s[i] = 0;
-	const uint32_t* c1 = cols + col_words;
-	for (size_t x = (size_t)blockIdx.x * kT + threadIdx.x; x < h; x += (size_t)gridDim.x * kT) {
-		const Qm l0 = q_ld(cols + 4 * x), u0 = q_ld(cols + 4 * (x + h));
-		const Qm l1 = q_ld(c1 + 4 * x), u1 = q_ld(c1 + 4 * (x + h));
-		const Qm p[3] = {q_mul(l0, l1), q_mul(u0, u1), q_mul(q_add(q_sub(u0, l0), u0), q_add(q_sub(u1, l1), u1))};
-#pragma unroll
-		for (int k = 0; k < 3; k++) {
-			s[4 * k] += p[k].lo.a;
-			s[4 * k + 1] += p[k].lo.b;
-			s[4 * k + 2] += p[k].hi.a;
-			s[4 * k + 3] += p[k].hi.b;
-		}
+	for (int k = 0; k < 3; k++) {
+		s[4 * k] += p[k].lo.a;
+		s[4 * k + 1] += p[k].lo.b;
+		s[4 * k + 2] += p[k].hi.a;
+		s[4 * k + 3] += p[k].hi.b;
 	}
+}
+
+// Block sums -> one device atomic per value (acc is cleared and read back around the launch).
+__device__ inline void qm_flush(unsigned long long (&s)[12], unsigned long long* acc) {
 	__shared__ unsigned long long red[kT / 64][12];
 #pragma unroll
 	for (int i = 0; i < 12; i++) {
@@ -125,6 +124,48 @@ __global__ __launch_bounds__(kT) void qm_messages(const uint32_t* cols, size_t c
 		for (int w = 0; w < kT / 64; w++) v += red[w][threadIdx.x];
 		if (v) atomicAdd(acc + threadIdx.x, v);
 	}
+}
+
+// round messages: lanes stride over x < h; exact u64 component sums -> one atomic per value per WG
+__global__ __launch_bounds__(kT) void qm_messages(const uint32_t* cols, size_t col_words, size_t h,
+                                                  unsigned long long* acc) {
+	unsigned long long s[12];
+#pragma unroll
+	for (int i = 0; i < 12; i++) s[i] = 0;
+	const uint32_t* c1 = cols + col_words;
+	for (size_t x = (size_t)blockIdx.x * kT + threadIdx.x; x < h; x += (size_t)gridDim.x * kT) {
+		qm_accumulate(s, q_ld(cols + 4 * x), q_ld(cols + 4 * (x + h)), q_ld(c1 + 4 * x), q_ld(c1 + 4 * (x + h)));
+	}
+	qm_flush(s, acc);
+}
+
+// fold(r) of the previous round fused with this round's messages: with the old half H = 2 h,
+// lane x < h reads old rows x, x + h, x + H, x + h + H of each column, writes the folded rows x
+// and x + h in place (disjoint from every other lane's reads) and accumulates the messages of
+// the pair (x, x + h). One pass instead of two: reads 2 x 32 B, writes 2 x 16 B per pair.
+__global__ __launch_bounds__(kT) void qm_fold_messages(uint32_t* cols, size_t col_words, size_t h, uint4 r4,
+                                                       unsigned long long* acc) {
+	const Qm r = {{r4.x, r4.y}, {r4.z, r4.w}};
+	unsigned long long s[12];
+#pragma unroll
+	for (int i = 0; i < 12; i++) s[i] = 0;
+	uint32_t* c1 = cols + col_words;
+	const size_t H = 2 * h;
+	for (size_t x = (size_t)blockIdx.x * kT + threadIdx.x; x < h; x += (size_t)gridDim.x * kT) {
+		Qm l[2], u[2];
+#pragma unroll
+		for (int j = 0; j < 2; j++) {
+			uint32_t* c = j ? c1 : cols;
+			const Qm a = q_ld(c + 4 * x), b = q_ld(c + 4 * (x + h));
+			const Qm aH = q_ld(c + 4 * (x + H)), bH = q_ld(c + 4 * (x + h + H));
+			l[j] = q_add(a, q_mul(q_sub(aH, a), r));
+			u[j] = q_add(b, q_mul(q_sub(bH, b), r));
+			q_st(c + 4 * x, l[j]);
+			q_st(c + 4 * (x + h), u[j]);
+		}
+		qm_accumulate(s, l[0], u[0], l[1], u[1]);
+	}
+	qm_flush(s, acc);
 }
 
 // fold: f(x) <- f(x) + r (f(x+h) - f(x)) for both columns, x < h
@@ -152,7 +193,7 @@ struct DevScope {
 
 static unsigned grid_for(const bn_qm31_sumcheck* S, size_t items) {
 	const size_t want = (items + kT - 1) / kT;
-	return (unsigned)std::max<size_t>(1, std::min<size_t>(want, (size_t)S->cus * 8));
+	return (unsigned)std::max<size_t>(1, std::min<size_t>(want, (size_t)S->cus * S->wg_per_cu));
 }
 
 }  // namespace
@@ -182,6 +223,7 @@ extern "C" int bn_qm31_sumcheck_create(int device, int num_vars, const uint32_t*
 	int cus = 0;
 	if (e == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
 		S->cus = std::max(cus, 1);
+	if (const char* v = getenv("BN_QM_WG_PER_CU")) S->wg_per_cu = std::max(1, atoi(v));
 	if (e == hipSuccess) {
 		// QM31(uint32_t) assumes values < p; reduce whatever was passed
 		hipLaunchKernelGGL(qm_reduce, dim3(grid_for(S, words)), dim3(kT), 0, S->stream, S->cols, words);
@@ -196,6 +238,16 @@ extern "C" int bn_qm31_sumcheck_create(int device, int num_vars, const uint32_t*
 	return BN_OK;
 }
 
+// A deferred fold not followed by round_messages (fold twice, or the last round) runs alone.
+static int apply_pending(bn_qm31_sumcheck* S) {
+	if (!S->pending) return BN_OK;
+	const size_t h = S->cur, col_words = ((size_t)4) << S->num_vars;  // cur is already the folded size
+	hipLaunchKernelGGL(qm_fold, dim3(grid_for(S, 2 * h)), dim3(kT), 0, S->stream, S->cols, col_words, h, S->pend_r);
+	BN_HIP(hipGetLastError());
+	S->pending = false;
+	return BN_OK;
+}
+
 // this_round_messages(points) (sumcheck.cuh:46-86): points 0, 1, 2 as 3 x 4 canonical words.
 extern "C" int bn_qm31_sumcheck_round_messages(bn_qm31_sumcheck* S, uint32_t* points) {
 	BN_CHECK_ARG(S != nullptr && points != nullptr, "NULL argument");
@@ -203,7 +255,13 @@ extern "C" int bn_qm31_sumcheck_round_messages(bn_qm31_sumcheck* S, uint32_t* po
 	DevScope ds(S->device);
 	const size_t h = S->cur / 2, col_words = ((size_t)4) << S->num_vars;
 	BN_HIP(hipMemsetAsync(S->acc, 0, 12 * sizeof(unsigned long long), S->stream));
-	hipLaunchKernelGGL(qm_messages, dim3(grid_for(S, h)), dim3(kT), 0, S->stream, S->cols, col_words, h, S->acc);
+	if (S->pending) {
+		hipLaunchKernelGGL(qm_fold_messages, dim3(grid_for(S, h)), dim3(kT), 0, S->stream, S->cols, col_words, h,
+		                   S->pend_r, S->acc);
+		S->pending = false;
+	} else {
+		hipLaunchKernelGGL(qm_messages, dim3(grid_for(S, h)), dim3(kT), 0, S->stream, S->cols, col_words, h, S->acc);
+	}
 	BN_HIP(hipGetLastError());
 	BN_HIP(hipMemcpyAsync(S->h_acc, S->acc, 12 * sizeof(unsigned long long), hipMemcpyDeviceToHost, S->stream));
 	BN_HIP(hipStreamSynchronize(S->stream));
@@ -217,14 +275,11 @@ extern "C" int bn_qm31_sumcheck_fold(bn_qm31_sumcheck* S, const uint32_t* challe
 	BN_CHECK_ARG(S != nullptr && challenge != nullptr, "NULL argument");
 	BN_CHECK_ARG(S->round < S->num_vars, "all %d rounds are done", S->num_vars);
 	DevScope ds(S->device);
-	const size_t h = S->cur / 2, col_words = ((size_t)4) << S->num_vars;
-	uint4 r;
-	r.x = challenge[0] % 0x7fffffffu;
-	r.y = challenge[1] % 0x7fffffffu;
-	r.z = challenge[2] % 0x7fffffffu;
-	r.w = challenge[3] % 0x7fffffffu;
-	hipLaunchKernelGGL(qm_fold, dim3(grid_for(S, 2 * h)), dim3(kT), 0, S->stream, S->cols, col_words, h, r);
-	BN_HIP(hipGetLastError());
+	const size_t h = S->cur / 2;
+	if (int rc = apply_pending(S)) return rc;
+	// deferred: the next round_messages fuses it (qm_fold_messages); final_values applies it alone
+	S->pend_r = make_uint4(challenge[0] % kM, challenge[1] % kM, challenge[2] % kM, challenge[3] % kM);
+	S->pending = true;
 	S->cur = h;
 	S->round++;
 	return BN_OK;
@@ -236,6 +291,7 @@ extern "C" int bn_qm31_sumcheck_final_values(bn_qm31_sumcheck* S, uint32_t* out 
 	BN_CHECK_ARG(S->round == S->num_vars, "only after all %d rounds (at round %d)", S->num_vars, S->round);
 	DevScope ds(S->device);
 	const size_t col_words = ((size_t)4) << S->num_vars;
+	if (int rc = apply_pending(S)) return rc;
 	BN_HIP(hipMemcpyAsync(out, S->cols, 16, hipMemcpyDeviceToHost, S->stream));
 	BN_HIP(hipMemcpyAsync(out + 4, S->cols + col_words, 16, hipMemcpyDeviceToHost, S->stream));
 	BN_HIP(hipStreamSynchronize(S->stream));

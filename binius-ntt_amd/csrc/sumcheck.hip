@@ -314,7 +314,7 @@ struct DeviceScope {
 	}
 	~DeviceScope() {
 		int cur = -1;
-		if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) hipSetDevice(prev);
+		if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
 	}
 };
 
@@ -393,11 +393,11 @@ int sc_common_init(bn_sumcheck* sc) {
 
 void sc_free(bn_sumcheck* sc) {
 	if (!sc) return;
-	if (sc->stream) hipStreamSynchronize(sc->stream);
-	if (sc->cols) hipFree(sc->cols);
-	if (sc->acc) hipFree(sc->acc);
-	if (sc->h_acc) hipHostFree(sc->h_acc);
-	if (sc->stream) hipStreamDestroy(sc->stream);
+	if (sc->stream) (void)hipStreamSynchronize(sc->stream);
+	if (sc->cols) (void)hipFree(sc->cols);
+	if (sc->acc) (void)hipFree(sc->acc);
+	if (sc->h_acc) (void)hipHostFree(sc->h_acc);
+	if (sc->stream) (void)hipStreamDestroy(sc->stream);
 	delete sc;
 }
 
@@ -572,7 +572,7 @@ extern "C" int bn_sumcheck_import_gathered(bn_sumcheck* sc, const uint32_t* word
 	hipError_t e = hipMemcpyAsync(cols, host.data(), sizeof(uint32_t) * host.size(), hipMemcpyHostToDevice, sc->stream);
 	if (e == hipSuccess) e = hipStreamSynchronize(sc->stream);
 	if (e != hipSuccess) {
-		hipFree(cols);
+		(void)hipFree(cols);
 		BN_FAIL(BN_ERR_HIP, "uploading gathered state: %s", hipGetErrorString(e));
 	}
 	BN_HIP(hipFree(sc->cols));

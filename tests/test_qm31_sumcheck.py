@@ -109,3 +109,23 @@ def test_gpu_rejects_bad_arguments(dev):
     sc.fold(PF.QM31(3))
     with pytest.raises(B.BnError):
         sc.this_round_messages()
+
+
+@pytest.mark.gpu
+def test_gpu_folds_without_messages(dev):
+    # fold is deferred and fused into the next round's messages; consecutive folds and a final
+    # fold must still apply in order
+    import binius_ntt_amd.prime_field as PF
+    n = 11
+    ev = _random_evals(n, 77)
+    ch = np.random.default_rng(78).integers(0, O.M31_P, size=(n, 4), dtype=np.uint64).astype(np.uint32)
+    want = O.qm31_sumcheck_run(ev, n, ch)
+    sc = PF.Sumcheck(n, ev.reshape(-1, 4))
+    for i in range(n):
+        if i % 3 == 1:
+            got = np.stack([q.words() for q in sc.this_round_messages()])
+            assert np.array_equal(got, want[i]), i
+        sc.fold(PF.QM31(list(ch[i])))
+    f0, f1 = sc.final_values()
+    _, finals = _gpu_run(n, ev, ch)
+    assert (f0.words().tolist(), f1.words().tolist()) == (finals[0].tolist(), finals[1].tolist())
