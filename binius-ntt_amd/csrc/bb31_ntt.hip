@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "common.hpp"
@@ -202,9 +203,135 @@ __global__ __launch_bounds__(kThreads) void bb_pass(BbArgs A) {
 	}
 }
 
+// Register-resident variant for the multi-pass roles (0, 1) and M = m in [6, 9]: the same tile,
+// twiddles and output as bb_pass, but a thread holds E = R/8 elements of one column, rows
+// t + 8i, so the radix-2 stages with half >= 8 run in registers; one LDS exchange regroups the
+// column into runs of 8 rows for the last three stages. LDS traffic per tile: the exchange and the
+// output gather, instead of two reads and two writes per element per stage.
+template <int ROLE, int M>
+__global__ __launch_bounds__(kThreads) void bb_pass_r(BbArgs A) {
+	constexpr int R = 1 << M, E = R / 8;
+	extern __shared__ uint32_t lds[];
+	const BbPass& ps = A.p;
+	const int tid = threadIdx.x;
+	const size_t b = blockIdx.y;
+	const uint32_t* src = A.src + b * A.n;
+	uint32_t* dst = A.dst + b * A.n;
+	const size_t tile = blockIdx.x;
+	size_t q = 0, cb = 0, kb = 0, gpos = 0, gout = 0;
+	if (ROLE == 0) {
+		const size_t ncb = ((size_t)1 << ps.log_mp) / kCols;
+		q = tile / ncb;
+		cb = tile % ncb;
+	} else {
+		const size_t nkb = ((size_t)1 << ps.m1) / kCols;
+		size_t g = tile / nkb;
+		kb = tile % nkb;
+		for (int i = 0; i < ps.ndig; i++) {
+			const size_t d = g & (((size_t)1 << ps.mdig[i]) - 1);
+			g >>= ps.mdig[i];
+			gpos += d << ps.log_pos[i];
+			gout += d << ps.log_out[i];
+		}
+	}
+	// ROLE 0 reads rows of 32 contiguous columns (lanes along c); ROLE 1's rows are contiguous,
+	// so 8 lanes walk 8 consecutive rows of one column
+	const int c = ROLE == 0 ? tid % kCols : tid / 8;
+	const int t = ROLE == 0 ? tid / kCols : tid % 8;
+	auto src_addr = [&](int r) -> size_t {
+		if (ROLE == 0) {
+			const size_t j = (q << ps.log_sub) + ((size_t)r << ps.log_mp) + cb * kCols + c;
+			return ps.bitrev_in ? (size_t)rev_bits((uint32_t)j, A.log_n) : j;
+		}
+		return ((kb * kCols + c) << (A.log_n - ps.m1)) + gpos + r;
+	};
+	uint32_t* twl = lds + R * kCols;
+	for (int i = tid; i < R / 2; i += kThreads) twl[i] = wpow(A, (uint32_t)i << (A.log_n - M));
+	uint32_t x[E];
+#pragma unroll
+	for (int i = 0; i < E; i++) x[i] = bb_reduce(src[src_addr(t + 8 * i)]);
+	__syncthreads();  // twl
+	// stages half = 2^s >= 8: rows t + 8i and t + 8i + half are both in this thread (i + half/8)
+#pragma unroll
+	for (int s = M - 1; s >= 3; s--) {
+		const int hi = 1 << (s - 3);
+#pragma unroll
+		for (int i = 0; i < E; i++) {
+			if (i & hi) continue;
+			const uint32_t u = x[i], v = x[i + hi];
+			const int k = (t + 8 * i) & ((1 << s) - 1);
+			x[i] = bb_add(u, v);
+			const uint32_t d = bb_sub(u, v);
+			x[i + hi] = k ? mont(d, twl[k << (M - 1 - s)]) : d;
+		}
+	}
+	// regroup: this thread takes rows 8g + j (j < 8) for g = t + 8u
+#pragma unroll
+	for (int i = 0; i < E; i++) lds[(t + 8 * i) * kCols + c] = x[i];
+	__syncthreads();
+#pragma unroll
+	for (int u = 0; u < E / 8; u++)
+#pragma unroll
+		for (int j = 0; j < 8; j++) x[8 * u + j] = lds[(8 * (t + 8 * u) + j) * kCols + c];
+#pragma unroll
+	for (int s = 2; s >= 0; s--) {
+		const int half = 1 << s;
+#pragma unroll
+		for (int i = 0; i < E; i++) {
+			const int j = i & 7;
+			if (j & half) continue;
+			const uint32_t u = x[i], v = x[i + half];
+			const int k = j & (half - 1);
+			x[i] = bb_add(u, v);
+			const uint32_t d = bb_sub(u, v);
+			x[i + half] = k ? mont(d, twl[k << (M - 1 - s)]) : d;
+		}
+	}
+#pragma unroll
+	for (int u = 0; u < E / 8; u++)
+#pragma unroll
+		for (int j = 0; j < 8; j++) lds[(8 * (t + 8 * u) + j) * kCols + c] = x[8 * u + j];
+	__syncthreads();
+	// output: as bb_pass (row k sits at LDS row rev_M(k))
+	if (ROLE == 0) {
+		const int cc = tid % kCols, k0 = tid / kCols;
+		const size_t cf = cb * kCols + cc;
+		const size_t msk = ((size_t)1 << ps.log_sub) - 1;
+		const int sh = A.log_n - ps.log_sub;
+		uint32_t tw = wpow(A, (uint32_t)(((cf * (size_t)k0) & msk) << sh));
+		const uint32_t step = wpow(A, (uint32_t)(((cf * (size_t)(kThreads / kCols)) & msk) << sh));
+#pragma unroll 4
+		for (int k = k0; k < R; k += kThreads / kCols) {
+			const uint32_t v = mont(lds[rev_bits((uint32_t)k, M) * kCols + cc], tw);
+			dst[(q << ps.log_sub) + ((size_t)k << ps.log_mp) + cf] = v;
+			tw = mont(tw, step);
+		}
+	} else {
+#pragma unroll 4
+		for (int u = tid; u < R * kCols; u += kThreads) {
+			const int k = u / kCols, cc = u % kCols;
+			dst[(kb * kCols + cc) + gout + ((size_t)k << (A.log_n - M))] = lds[rev_bits((uint32_t)k, M) * kCols + cc];
+		}
+	}
+}
+
 template <int ROLE>
 static const void* pass_fn() {
 	return (const void*)bb_pass<ROLE>;
+}
+
+static const void* pass_r_fn(int role, int m) {
+	static const void* r[2][4] = {
+	    {(const void*)bb_pass_r<0, 6>, (const void*)bb_pass_r<0, 7>, (const void*)bb_pass_r<0, 8>, (const void*)bb_pass_r<0, 9>},
+	    {(const void*)bb_pass_r<1, 6>, (const void*)bb_pass_r<1, 7>, (const void*)bb_pass_r<1, 8>, (const void*)bb_pass_r<1, 9>}};
+	return r[role][m - 6];
+}
+
+// the register variant where it applies (roles 0/1, m in 6..9); BN_BB_LDS=1 forces bb_pass (A/B)
+static const void* pass_fn_for(const BbPass& p) {
+	static const bool lds_only = getenv("BN_BB_LDS") != nullptr;
+	if (!lds_only && p.role != 2 && p.m >= 6 && p.m <= 9) return pass_r_fn(p.role, p.m);
+	return p.role == 0 ? pass_fn<0>() : p.role == 1 ? pass_fn<1>() : pass_fn<2>();
 }
 
 static std::vector<BbPass> bb_passes(const bn_bb31_ntt_plan* P, bool bitrev_in) {
@@ -305,7 +432,8 @@ extern "C" int bn_bb31_ntt_plan_create(int device, uint32_t generator, int log_g
 	if (e == hipSuccess) e = hipMalloc(&P->wtab, tab.size() * sizeof(uint32_t));
 	if (e == hipSuccess) e = hipMemcpy(P->wtab, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
 	if (e == hipSuccess)
-		for (const void* f : {pass_fn<0>(), pass_fn<1>(), pass_fn<2>()})
+		for (const void* f : {pass_fn<0>(), pass_fn<1>(), pass_fn<2>(), pass_r_fn(0, 6), pass_r_fn(0, 7), pass_r_fn(0, 8),
+		                      pass_r_fn(0, 9), pass_r_fn(1, 6), pass_r_fn(1, 7), pass_r_fn(1, 8), pass_r_fn(1, 9)})
 			if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, ((1 << kMaxM) * kCols + (1 << 12)) * 4);
 	hipSetDevice(prev);
 	if (e != hipSuccess) {
@@ -368,7 +496,7 @@ static int bb_forward(bn_bb31_ntt_plan* P, const uint32_t* d_in, uint32_t* d_out
 			W = (1 << p.m) * kCols;
 		}
 		void* args[] = {&A};
-		const void* fn = p.role == 0 ? pass_fn<0>() : p.role == 1 ? pass_fn<1>() : pass_fn<2>();
+		const void* fn = pass_fn_for(p);
 		BN_HIP(hipLaunchKernel(fn, dim3((unsigned)tiles, (unsigned)batch), dim3(kThreads), args,
 		                       ((size_t)W + ((size_t)1 << p.m) / 2) * 4, st));
 	}
