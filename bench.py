@@ -2,8 +2,8 @@
 """Headline benchmark: 2^24-point GF(2^128) additive NTT (BASELINE.json configs[...], north star).
 
 One "step" = one full forward transform (log_h = 24, log_rate = 0) of a device-resident,
-synthetic GF(2^128) vector (limb 0 = std::mt19937(0xdeadbeef+24), limbs 1..3 = mt19937_64
-streams) into a separate device output buffer.
+synthetic GF(2^128) vector (numpy PCG64, seed 0xdeadbeef + 24 + rank) into a separate device
+output buffer. The oracle (test infrastructure) is used only by the cpu_baseline leg.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--log-h 24] [--no-cpu]
 
@@ -23,7 +23,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "binius-ntt_amd", "python"))
 
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-VALU_PEAK_TOPS = 78.6        # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz 32-bit VALU ops/s
 
 
 def parse():
@@ -50,6 +49,16 @@ def cpu_baseline(log_h):
                       "algorithm, 1 thread, %.2f s" % (log_h, dt)}
 
 
+def load_valu_insts():
+    """SQ_INSTS_VALU per launch of each pass kernel from the committed PMC summary (rocprofv3)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")) as f:
+            d = json.load(f)
+        return [v.get("SQ_INSTS_VALU") for k, v in sorted(d.items(), key=lambda kv: kv[0])]
+    except (OSError, ValueError):
+        return None
+
+
 def load_pmc(log_h):
     """HBM traffic per launch from the committed rocprofv3 PMC summary, if present."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -59,6 +68,18 @@ def load_pmc(log_h):
         return d.get(str(log_h))
     except (OSError, ValueError):
         return None
+
+
+VALU_PEAK_WAVE_INSTS = 256 * 4 * 0.5 * 2.4e9
+
+
+def valu_block(dom, dom_ms):
+    insts = load_valu_insts()
+    if not insts or dom is None or dom >= len(insts) or not insts[dom]:
+        return None
+    rate = insts[dom] / (dom_ms * 1e-3)
+    return {"insts_per_launch": insts[dom], "achieved": rate, "peak": VALU_PEAK_WAVE_INSTS,
+            "unit": "wave64 instructions/s", "frac": rate / VALU_PEAK_WAVE_INSTS}
 
 
 def main():
@@ -87,11 +108,10 @@ def main():
     log_h = a.log_h
     n = 1 << log_h
 
-    # synthetic input generated on the host by the seeded streams, resident in HBM before timing
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import _oracle as O
-    x = O.fill128(0xDEADBEEF + log_h + rank, 0x5EED0000 + 16 * rank, n)
-    d_in = torch.from_numpy(x.reshape(-1).view(np.int32)).to(dev)
+    # synthetic input generated on the host, resident in HBM before timing
+    x = np.random.default_rng(0xDEADBEEF + log_h + rank).integers(0, 2**32, size=4 * n, dtype=np.uint64)
+    d_in = torch.from_numpy(x.astype(np.uint32).view(np.int32)).to(dev)
+    del x
     d_out = torch.empty_like(d_in)
     ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(7), device=local))
     stream = torch.cuda.current_stream(dev)
@@ -147,7 +167,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "gf2_128 (u32 limbs, bitwise)",
-            "data": "synthetic (seeded mt19937 / mt19937_64 limbs)",
+            "data": "synthetic (numpy PCG64 seeded limbs)",
             "config": {"workload": "additive NTT over GF(2^128), log_h=%d, log_rate=0, one transform per GPU"
                                    % log_h, "log_h": log_h, "log_rate": 0, "field": "GF(2^128)",
                        "kernel_variant": ntt.variant(), "parallelism": "independent transform per rank"},
@@ -164,6 +184,10 @@ def main():
                 "pass_ms": kind_ms,
                 "transform_frac": transform_gbps / HBM_PEAK_GBPS,
             },
+            # the pass kernels are VALU-issue bound: wave-instructions per launch
+            # (SQ_INSTS_VALU, committed PMC run) / the live hipEvent duration vs the issue peak of
+            # 256 CU x 4 SIMD x 0.5 wave64 instructions/cycle x 2.4 GHz
+            "valu": valu_block(dom, dom_ms),
         }
         if not a.no_cpu and world == 1:
             res["cpu_baseline"] = cpu_baseline(a.cpu_log_h)
