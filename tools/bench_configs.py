@@ -188,9 +188,9 @@ def qm_line(dev, out, nvars, reps=3):
         best = dt if best is None else min(best, dt)
     out({"config": "qm", "workload": "QM31 sumcheck 2 x 2^%d, d=2, all rounds" % nvars,
          "value": (1 << nvars) / best, "unit": "evals/s", "ms": best * 1e3,
-         # per round over cur pairs: messages read 2 x 16 B x cur, fold reads the same and writes
-         # half; sum of cur over rounds ~ 2 x 2^N  ->  160 B per eval
-         "hbm_gbps_algorithmic": 160 * (1 << nvars) / best / 1e9})
+         # per round over cur evals: the fused fold+messages pass reads 2 x 16 B x cur and writes
+         # half of that; sum of cur over rounds ~ 2 x 2^N  ->  96 B per eval
+         "hbm_gbps_algorithmic": 96 * (1 << nvars) / best / 1e9})
 
 
 def main():
