@@ -1,7 +1,11 @@
 """The C++ host mirror (binius-ntt_amd/host/ulvt: AdditiveNTT<T,P>, NTTData, AdditiveNTTConf,
-FanPaarTowerField, BitsliceUtils, Sumcheck<N,d,T>) builds against the C-ABI alone (CPU), and on
-the GPU runs the reference's own test flows (tests/cpp/test_surface.cpp): the GF(2^32) MD5 table
-of test_ntt.cu, GF(2^128) vs the oracle, and the sumcheck verifier loop of test.cu."""
+FanPaarTowerField, BitsliceUtils, Sumcheck<N,d,T>; and the prime-field siblings NTT<BB31>,
+NTTConfRad2, BB31, QM31, Sumcheck<N>, interpolate_at) builds against the C-ABI alone (CPU), and on
+the GPU runs the reference's own test flows (tests/cpp/test_surface.cpp: the GF(2^32) MD5 table
+of test_ntt.cu, GF(2^128) vs the oracle, the sumcheck verifier loop of test.cu;
+tests/cpp/test_prime_field.cpp: the BabyBear MD5 table and round trip of test_ntt.cu and the
+"Prime Field Sumcheck Test")."""
+import json
 import os
 import subprocess
 
@@ -13,11 +17,14 @@ ORACLE = os.path.join(ROOT, "oracle")
 BIN = os.path.join(ROOT, "tests", "cpp", "build", "test_surface")
 
 
-def _build():
-    os.makedirs(os.path.dirname(BIN), exist_ok=True)
+PRIME_BIN = os.path.join(ROOT, "tests", "cpp", "build", "test_prime_field")
+
+
+def _build(src="test_surface.cpp", out=BIN):
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-Wextra",
            "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "binius-ntt_amd", "host", "ulvt"),
-           os.path.join(ROOT, "tests", "cpp", "test_surface.cpp"), "-o", BIN,
+           os.path.join(ROOT, "tests", "cpp", src), "-o", out,
            "-L", LIBDIR, "-lbinius_ntt_amd", "-L", ORACLE, "-loracle",
            "-Wl,-rpath," + LIBDIR, "-Wl,-rpath," + ORACLE, "-Wl,--allow-shlib-undefined"]
     subprocess.check_call(cmd)
@@ -38,6 +45,8 @@ def _build_bench():
 def test_cpp_mirror_builds_against_the_c_abi():
     _build()
     assert os.path.exists(BIN)
+    _build("test_prime_field.cpp", PRIME_BIN)
+    assert os.path.exists(PRIME_BIN)
     _build_bench()
     assert os.path.exists(BENCH)
 
@@ -69,3 +78,22 @@ def test_cpp_mirror_runs_reference_flows(ntt_md5):
                 n += 1
     assert n >= 30
     assert not [l for l in out if l.startswith("FAIL")]
+
+
+@pytest.mark.gpu
+def test_cpp_prime_field_mirror_runs_reference_flows():
+    _build("test_prime_field.cpp", PRIME_BIN)
+    with open(os.path.join(ROOT, "tests", "golden", "bb31_ntt_md5.json")) as f:
+        want = json.load(f)["hashes"]
+    p = subprocess.run([PRIME_BIN], capture_output=True, text=True, timeout=300)
+    out = p.stdout.splitlines()
+    assert p.returncode == 0, p.stdout + p.stderr
+    n = 0
+    for line in out:
+        if line.startswith("bbmd5 "):
+            _, log_n, h = line.split()
+            assert h == want[int(log_n)], line
+            n += 1
+    assert n == 22
+    assert not [l for l in out if l.startswith("FAIL")]
+    assert len([l for l in out if l.startswith("ok Prime Field Sumcheck Test")]) == 3
