@@ -26,11 +26,12 @@ struct bn_qm31_sumcheck {
 	int round = 0;
 	size_t cur = 0;  // evaluations per column still live
 	uint32_t* cols = nullptr;  // 2 columns x 2^N x 4 words
-	unsigned long long* acc = nullptr;  // 12 x u64 (points 0..2 x 4 components)
+	unsigned long long* acc = nullptr;  // 2 x 12 u64 (points 0..2 x 4 components), alternating rounds
 	unsigned long long* h_acc = nullptr;  // pinned
 	hipStream_t stream = nullptr;
 	int cus = 256;
 	int wg_per_cu = 8;  // grid cap (BN_QM_WG_PER_CU overrides, for tuning)
+	int par = 0;  // accumulator set of the next round_messages
 	bool pending = false;  // a fold(r) not yet applied to cols (fused into the next round's messages)
 	uint4 pend_r = {0, 0, 0, 0};
 };
@@ -103,8 +104,11 @@ __device__ inline void qm_accumulate(unsigned long long (&s)[12], Qm l0, Qm u0, 
 	}
 }
 
-// Block sums -> one device atomic per value (acc is cleared and read back around the launch).
-__device__ inline void qm_flush(unsigned long long (&s)[12], unsigned long long* acc) {
+// Block sums -> one device atomic per value. Rounds alternate between two accumulator sets:
+// this round's workgroup 0 clears the other set (last read back by the previous round's copy,
+// which is ordered before this launch), so no memset is queued per round.
+__device__ inline void qm_flush(unsigned long long (&s)[12], unsigned long long* acc, unsigned long long* clr) {
+	if (blockIdx.x == 0 && threadIdx.x < 12) clr[threadIdx.x] = 0;
 	__shared__ unsigned long long red[kT / 64][12];
 #pragma unroll
 	for (int i = 0; i < 12; i++) {
@@ -128,7 +132,7 @@ __device__ inline void qm_flush(unsigned long long (&s)[12], unsigned long long*
 
 // round messages: lanes stride over x < h; exact u64 component sums -> one atomic per value per WG
 __global__ __launch_bounds__(kT) void qm_messages(const uint32_t* cols, size_t col_words, size_t h,
-                                                  unsigned long long* acc) {
+                                                  unsigned long long* acc, unsigned long long* clr) {
 	unsigned long long s[12];
 #pragma unroll
 	for (int i = 0; i < 12; i++) s[i] = 0;
@@ -136,7 +140,7 @@ __global__ __launch_bounds__(kT) void qm_messages(const uint32_t* cols, size_t c
 	for (size_t x = (size_t)blockIdx.x * kT + threadIdx.x; x < h; x += (size_t)gridDim.x * kT) {
 		qm_accumulate(s, q_ld(cols + 4 * x), q_ld(cols + 4 * (x + h)), q_ld(c1 + 4 * x), q_ld(c1 + 4 * (x + h)));
 	}
-	qm_flush(s, acc);
+	qm_flush(s, acc, clr);
 }
 
 // fold(r) of the previous round fused with this round's messages: with the old half H = 2 h,
@@ -144,7 +148,7 @@ __global__ __launch_bounds__(kT) void qm_messages(const uint32_t* cols, size_t c
 // and x + h in place (disjoint from every other lane's reads) and accumulates the messages of
 // the pair (x, x + h). One pass instead of two: reads 2 x 32 B, writes 2 x 16 B per pair.
 __global__ __launch_bounds__(kT) void qm_fold_messages(uint32_t* cols, size_t col_words, size_t h, uint4 r4,
-                                                       unsigned long long* acc) {
+                                                       unsigned long long* acc, unsigned long long* clr) {
 	const Qm r = {{r4.x, r4.y}, {r4.z, r4.w}};
 	unsigned long long s[12];
 #pragma unroll
@@ -165,7 +169,7 @@ __global__ __launch_bounds__(kT) void qm_fold_messages(uint32_t* cols, size_t co
 		}
 		qm_accumulate(s, l[0], u[0], l[1], u[1]);
 	}
-	qm_flush(s, acc);
+	qm_flush(s, acc, clr);
 }
 
 // fold: f(x) <- f(x) + r (f(x+h) - f(x)) for both columns, x < h
@@ -217,7 +221,8 @@ extern "C" int bn_qm31_sumcheck_create(int device, int num_vars, const uint32_t*
 	const size_t words = 2 * S->cur * 4;
 	hipError_t e = hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking);
 	if (e == hipSuccess) e = hipMalloc(&S->cols, words * 4);
-	if (e == hipSuccess) e = hipMalloc(&S->acc, 12 * sizeof(unsigned long long));
+	if (e == hipSuccess) e = hipMalloc(&S->acc, 24 * sizeof(unsigned long long));
+	if (e == hipSuccess) e = hipMemsetAsync(S->acc, 0, 24 * sizeof(unsigned long long), S->stream);
 	if (e == hipSuccess) e = hipHostMalloc(&S->h_acc, 12 * sizeof(unsigned long long), hipHostMallocDefault);
 	if (e == hipSuccess) e = hipMemcpyAsync(S->cols, evals, words * 4, hipMemcpyHostToDevice, S->stream);
 	int cus = 0;
@@ -254,16 +259,18 @@ extern "C" int bn_qm31_sumcheck_round_messages(bn_qm31_sumcheck* S, uint32_t* po
 	BN_CHECK_ARG(S->round < S->num_vars, "all %d rounds are done", S->num_vars);
 	DevScope ds(S->device);
 	const size_t h = S->cur / 2, col_words = ((size_t)4) << S->num_vars;
-	BN_HIP(hipMemsetAsync(S->acc, 0, 12 * sizeof(unsigned long long), S->stream));
+	unsigned long long* acc = S->acc + 12 * S->par;
+	unsigned long long* clr = S->acc + 12 * (1 - S->par);
 	if (S->pending) {
 		hipLaunchKernelGGL(qm_fold_messages, dim3(grid_for(S, h)), dim3(kT), 0, S->stream, S->cols, col_words, h,
-		                   S->pend_r, S->acc);
+		                   S->pend_r, acc, clr);
 		S->pending = false;
 	} else {
-		hipLaunchKernelGGL(qm_messages, dim3(grid_for(S, h)), dim3(kT), 0, S->stream, S->cols, col_words, h, S->acc);
+		hipLaunchKernelGGL(qm_messages, dim3(grid_for(S, h)), dim3(kT), 0, S->stream, S->cols, col_words, h, acc, clr);
 	}
 	BN_HIP(hipGetLastError());
-	BN_HIP(hipMemcpyAsync(S->h_acc, S->acc, 12 * sizeof(unsigned long long), hipMemcpyDeviceToHost, S->stream));
+	BN_HIP(hipMemcpyAsync(S->h_acc, acc, 12 * sizeof(unsigned long long), hipMemcpyDeviceToHost, S->stream));
+	S->par ^= 1;
 	BN_HIP(hipStreamSynchronize(S->stream));
 	// QM31(uint64_t[4]) -> M31(uint64_t) (m31.cuh:21-24): the exact sum, reduced
 	for (int i = 0; i < 12; i++) points[i] = (uint32_t)(S->h_acc[i] % 0x7fffffffull);
