@@ -195,7 +195,8 @@ struct ScArgs {
 	int mode;           // 0 big, 1 in-batch pairs, 2 single element (cur == 1)
 	int kmax;           // points 0..kmax
 	uint32_t r[4];      // fold challenge
-	uint32_t* acc;      // (kmax + 1) x 4 words, XOR-accumulated
+	uint32_t* acc;      // (kmax + 1) x 4 words, XOR-accumulated (this round's set)
+	uint32_t* clr;      // the other accumulator set: cleared here for the next round
 	uint32_t kcol[kMaxD + 1][4];  // GF(2^4) products k * 2^a (interpolation point k)
 };
 
@@ -237,6 +238,9 @@ __global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
 	const Slot S{lds + qw * kQuadWords};
 	uint32_t* accL = lds + kQuadsPerWG * kQuadWords + 128;  // (kMaxD + 1) x 4 words
 	if (threadIdx.x < 4 * (kMaxD + 1)) accL[threadIdx.x] = 0;
+	// rounds alternate between two accumulator sets; the other set was last read back by the
+	// previous round's copy (ordered before this launch), so no memset is queued per round
+	if (blockIdx.x == 0 && threadIdx.x < 4 * (kMaxD + 1)) A.clr[threadIdx.x] = 0;
 	__syncthreads();
 	const int npts = A.kmax + 1;
 	const size_t item = (size_t)blockIdx.x * kQuadsPerWG + qw;
@@ -329,7 +333,8 @@ struct bn_sumcheck {
 	size_t cur = 0;         // evaluations per column held by this prover
 	size_t col_words = 0;   // words between columns (allocation)
 	uint32_t* cols = nullptr;
-	uint32_t* acc = nullptr;
+	uint32_t* acc = nullptr;    // 2 sets of 4 * (kMaxD + 1) words, alternating rounds
+	int par = 0;                // set used by the next round_messages
 	uint32_t* h_acc = nullptr;  // pinned host copy of acc (round messages)
 	hipStream_t stream = nullptr;
 	bool sharded_used = false;
@@ -359,14 +364,14 @@ int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 		A.n_pairs = 1;
 		A.kmax = 0;
 	}
-	A.acc = sc->acc;
+	A.acc = sc->acc + 4 * (kMaxD + 1) * sc->par;
+	A.clr = sc->acc + 4 * (kMaxD + 1) * (1 - sc->par);
 	if (fold) memcpy(A.r, r, 16);
 	for (int k = 0; k <= kMaxD; k++)
 		for (int a = 0; a < 4; a++) A.kcol[k][a] = (uint32_t)tw_mul((uint64_t)k, 1ull << a, 2);
 	// one item per quad: fold (column, pair), messages (pair, point)
 	const size_t items = fold ? (size_t)sc->d * A.n_pairs : A.n_pairs * (size_t)(A.kmax + 1);
 	const size_t grid = (items + kQuadsPerWG - 1) / kQuadsPerWG;
-	if (!fold) BN_HIP(hipMemsetAsync(sc->acc, 0, sizeof(uint32_t) * 4 * (kMaxD + 1), sc->stream));
 	void* args[] = {&A};
 	const void* fns[2][3] = {{(const void*)sc_messages<0>, (const void*)sc_messages<1>, (const void*)sc_messages<2>},
 							 {(const void*)sc_fold<0>, (const void*)sc_fold<1>, (const void*)sc_fold<2>}};
@@ -383,7 +388,8 @@ int sc_alloc(bn_sumcheck* sc, size_t col_words) {
 
 int sc_common_init(bn_sumcheck* sc) {
 	BN_HIP(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
-	BN_HIP(hipMalloc(&sc->acc, sizeof(uint32_t) * 4 * (kMaxD + 1)));
+	BN_HIP(hipMalloc(&sc->acc, sizeof(uint32_t) * 8 * (kMaxD + 1)));
+	BN_HIP(hipMemsetAsync(sc->acc, 0, sizeof(uint32_t) * 8 * (kMaxD + 1), sc->stream));
 	BN_HIP(hipHostMalloc((void**)&sc->h_acc, sizeof(uint32_t) * 4 * (kMaxD + 1), hipHostMallocDefault));
 	const void* fns[6] = {(const void*)sc_messages<0>, (const void*)sc_messages<1>, (const void*)sc_messages<2>,
 						  (const void*)sc_fold<0>,     (const void*)sc_fold<1>,     (const void*)sc_fold<2>};
@@ -591,7 +597,9 @@ extern "C" int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32
 	int rc = sc_launch(sc, false, nullptr);
 	if (rc != BN_OK) return rc;
 	const uint32_t* acc = sc->h_acc;
-	BN_HIP(hipMemcpyAsync(sc->h_acc, sc->acc, sizeof(uint32_t) * 4 * (kMaxD + 1), hipMemcpyDeviceToHost, sc->stream));
+	BN_HIP(hipMemcpyAsync(sc->h_acc, sc->acc + 4 * (kMaxD + 1) * sc->par, sizeof(uint32_t) * 4 * (kMaxD + 1),
+						  hipMemcpyDeviceToHost, sc->stream));
+	sc->par ^= 1;
 	BN_HIP(hipStreamSynchronize(sc->stream));
 	const int npts = sc->d + 1;
 	if (sc->cur == 1) {
