@@ -82,6 +82,24 @@ def valu_block(dom, dom_ms):
             "unit": "wave64 instructions/s", "frac": rate / VALU_PEAK_WAVE_INSTS}
 
 
+def apply_e2e(B, ntt, d_in, n, reps=3):
+    """Reference-semantics AdditiveNTT::apply (host buffers: H2D + transform + D2H, synchronous);
+    reported beside `value`, never as it."""
+    import numpy as np
+    host = d_in.cpu().numpy().view(np.uint32).reshape(n, 4)
+    inp = B.NTTData(n, B.DataOrder.IN_ORDER, 128, host)
+    out = B.NTTData(n, B.DataOrder.INVALID, 128)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        if not ntt.apply(inp, out):
+            return None
+        ts.append(time.perf_counter() - t0)
+    t = sorted(ts)[len(ts) // 2]
+    return {"ms": t * 1e3, "elements_per_s": n / t, "reps": reps,
+            "note": "AdditiveNTT.apply on pageable host buffers (PCIe-inclusive), median"}
+
+
 def main():
     a = parse()
     import numpy as np
@@ -189,6 +207,8 @@ def main():
             # 256 CU x 4 SIMD x 0.5 wave64 instructions/cycle x 2.4 GHz
             "valu": valu_block(dom, dom_ms),
         }
+        if world == 1:
+            res["apply_e2e"] = apply_e2e(B, ntt, d_in, n)
         if not a.no_cpu and world == 1:
             res["cpu_baseline"] = cpu_baseline(a.cpu_log_h)
         else:
