@@ -1,20 +1,31 @@
 #!/usr/bin/env python3
-"""Headline benchmark: 2^24-point GF(2^128) additive NTT (BASELINE.json configs[...], north star).
+"""Headline benchmark: 2^24-point GF(2^128) additive NTT (BASELINE.json north star), plus the
+config-5 multi-GPU workloads.
 
 One "step" = one full forward transform (log_h = 24, log_rate = 0) of a device-resident,
 synthetic GF(2^128) vector (numpy PCG64, seed 0xdeadbeef + 24 + rank) into a separate device
 output buffer. The oracle (test infrastructure) is used only by the cpu_baseline leg.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--log-h 24] [--no-cpu]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--log-h 24] [--no-cpu] [--no-c5]
 
-N > 1 is launched by torch.distributed.run: every rank transforms its own 2^24 vector
-(independent transforms = batched sharding, weak scaling, no data-path collective); the timed
-region is bracketed by barriers + synchronize and the max over ranks is reported. Rank 0
-prints one JSON line.
+--gpus N > 1 without a torch.distributed environment re-launches this script as a child
+`python -m torch.distributed.run --nproc-per-node N` (before anything touches the GPU) and exits
+with its status. Under torch.distributed every rank drives one GPU:
+  * headline: every rank transforms its own 2^24 vector (independent transforms = batched
+    sharding, weak scaling, no data-path collective); the timed region is bracketed by barriers +
+    synchronize and the max over ranks is reported;
+  * c5.batched_ntt: 256 x 2^20-point transforms split over the ranks (rank g owns a contiguous
+    slice, no collective; strong scaling over the fixed batch);
+  * c5.sumcheck: the 2^28-evaluation, d = 3 bitsliced sumcheck sharded by 32-element batch
+    (b mod world == rank); every round all-gathers the (d + 2) x 16 B partial messages and XORs
+    them (RCCL has no XOR reduction); the endgame gathers the last batches.
+Rank 0 prints one JSON line. BENCH_DIST_BACKEND=gloo rehearses the multi-rank path on fewer
+GPUs (ranks then share devices round-robin; collectives run on CPU tensors).
 """
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -23,6 +34,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "binius-ntt_amd", "python"))
 
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue peak: 256 CU x 4 SIMD x 0.5 wave64 instructions/cycle (SIMD-32) x 2.4 GHz
+VALU_PEAK_WAVE_INSTS = 256 * 4 * 0.5 * 2.4e9
 
 
 def parse():
@@ -32,97 +45,120 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log-h", type=int, default=24)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-log-h", type=int, default=24)
+    ap.add_argument("--no-c5", action="store_true", help="skip the config-5 legs")
+    ap.add_argument("--c5-log-n", type=int, default=20)
+    ap.add_argument("--c5-batch", type=int, default=256)
+    ap.add_argument("--c5-steps", type=int, default=3)
+    ap.add_argument("--sc-log-n", type=int, default=28)
+    ap.add_argument("--sc-d", type=int, default=3)
+    ap.add_argument("--sc-runs", type=int, default=2)
     return ap.parse_args()
 
 
-def cpu_baseline(log_h):
-    """Oracle (C restatement of the reference algorithm) on one transform: 1 thread (the
-    reported value), and the 4 limb-plane GF(2^32) transforms on 4 threads (`parallel`)."""
+def relaunch_if_needed(a):
+    """--gpus N without a torch.distributed environment: run N ranks as a child process group
+    (never exec: the parent has not touched the GPU, the child does) and exit with its status."""
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != a.gpus:
+            raise SystemExit("bench.py: --gpus %d disagrees with WORLD_SIZE=%d" % (a.gpus, world))
+        return
+    if a.gpus <= 1:
+        return
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = os.cpu_count()
+    threads = allowed
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        threads = min(threads, int(cap))  # the box's CPU share for one GPU
+    return model, os.cpu_count(), allowed, threads
+
+
+def cpu_baseline():
+    """The oracle (a C restatement of the reference algorithm, oracle/antt.c) on the GPU box's
+    own host cores: 1 thread and all usable threads, at 2^10, 2^20 and 2^24 points."""
+    import ctypes
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from concurrent.futures import ThreadPoolExecutor
     import numpy as np
     import _oracle as O
-    x = O.fill128(0xDEADBEEF + log_h, 0x5EED0000, 1 << log_h)
-    t0 = time.perf_counter()
-    O.antt128(x, log_h, 0)
-    dt = time.perf_counter() - t0
-    planes = [np.ascontiguousarray(x.reshape(-1, 4)[:, j]) for j in range(4)]
-    t1 = time.perf_counter()
-    with ThreadPoolExecutor(4) as ex:  # ctypes releases the GIL inside the oracle
-        list(ex.map(lambda p: O.antt32(p, log_h, 0), planes))
-    dt4 = time.perf_counter() - t1
-    return {"value": (1 << log_h) / dt, "unit": "elements/s", "cores": 1, "kind": "port",
-            "sample": "one 2^%d-point GF(2^128) additive NTT (r=0), oracle/ C port of the reference "
-                      "algorithm, 1 thread, %.2f s" % (log_h, dt),
-            "parallel": {"value": (1 << log_h) / dt4, "cores": 4,
-                         "sample": "same transform as 4 limb-plane GF(2^32) transforms on 4 threads, %.2f s"
-                                   % dt4}}
+    model, nproc, allowed, threads = cpu_info()
+    L = O.lib()
+    per_size = {}
+    total = 0.0
+    for log_h in (10, 20, 24):
+        x = O.fill128(0xDEADBEEF + log_h, 0x5EED0000, 1 << log_h)
+        out = np.zeros_like(x)
+        row = {}
+        for nt in (1, threads):
+            reps = max(1, min(200, (1 << 20) // (1 << log_h)))
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                L.orc_antt128_limbwise_mt(x.reshape(-1), out.reshape(-1), log_h, 0, nt)
+            dt = (time.perf_counter() - t0) / reps
+            total += dt * reps
+            row["threads_%d" % nt] = {"elements_per_s": (1 << log_h) / dt, "ms": dt * 1e3, "reps": reps}
+        per_size["2^%d" % log_h] = row
+    head = per_size["2^24"]["threads_%d" % threads]
+    return {"value": head["elements_per_s"], "unit": "elements/s", "cores": threads, "kind": "port",
+            "sample": "one 2^24-point GF(2^128) additive NTT (r=0) by oracle/antt.c (C port of the reference "
+                      "algorithm, butterflies of each stage split over %d pthreads); per_size has 1 thread and "
+                      "%d threads at 2^10/2^20/2^24 (%.1f s of CPU work in all)" % (threads, threads, total),
+            "cpu_model": model, "nproc": nproc, "cpus_allowed": allowed, "per_size": per_size}
 
 
-def load_valu_insts():
-    """SQ_INSTS_VALU per launch of each pass kernel from the committed PMC summary (rocprofv3)."""
+def load_pass_counters(log_h):
+    """SQ_INSTS_VALU per launch of each pass from the committed rocprofv3 PMC summary, keyed
+    by log_h and pass index (tools/pmc_summary.py); None if this layout was not profiled."""
     try:
-        with open(os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")) as f:
+        with open(os.path.join(ROOT, "profiles", "r02", "pmc_summary.json")) as f:
             d = json.load(f)
-        return [v.get("SQ_INSTS_VALU") for k, v in sorted(d.items(), key=lambda kv: kv[0])]
+        return d.get("log_h=%d" % log_h)
     except (OSError, ValueError):
         return None
 
 
-def load_pmc(log_h):
-    """HBM traffic per launch from the committed rocprofv3 PMC summary, if present."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def load_traffic(log_h):
+    """HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) per pass."""
     try:
-        with open(path) as f:
+        with open(os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")) as f:
             d = json.load(f)
-        return d.get(str(log_h))
+        return d.get("log_h=%d" % log_h)
     except (OSError, ValueError):
         return None
-
-
-VALU_PEAK_WAVE_INSTS = 256 * 4 * 0.5 * 2.4e9
-
-
-def valu_block(dom, dom_ms):
-    insts = load_valu_insts()
-    if not insts or dom is None or dom >= len(insts) or not insts[dom]:
-        return None
-    rate = insts[dom] / (dom_ms * 1e-3)
-    return {"insts_per_launch": insts[dom], "achieved": rate, "peak": VALU_PEAK_WAVE_INSTS,
-            "unit": "wave64 instructions/s", "frac": rate / VALU_PEAK_WAVE_INSTS}
-
-
-def apply_e2e(B, ntt, d_in, n, reps=3):
-    """Reference-semantics AdditiveNTT::apply (host buffers: H2D + transform + D2H, synchronous);
-    reported beside `value`, never as it (SURVEY.md §8d)."""
-    import numpy as np
-    host = d_in.cpu().numpy().view(np.uint32).reshape(n, 4)
-    inp = B.NTTData(n, B.DataOrder.IN_ORDER, 128, host)
-    out = B.NTTData(n, B.DataOrder.INVALID, 128)
-    ts = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        if not ntt.apply(inp, out):
-            return None
-        ts.append(time.perf_counter() - t0)
-    t = sorted(ts)[len(ts) // 2]
-    return {"ms": t * 1e3, "elements_per_s": n / t, "reps": reps,
-            "note": "AdditiveNTT.apply on pageable host buffers (PCIe-inclusive), median"}
 
 
 def main():
     a = parse()
+    relaunch_if_needed(a)
     import numpy as np
     import torch
     import torch.distributed as dist
     import binius_ntt_amd as B
+    from binius_ntt_amd import distributed as D
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; BENCH_DIST_BACKEND=gloo rehearses the multi-rank path on fewer GPUs
-    # (ranks then share devices round-robin; the timing all-reduce runs on CPU tensors)
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
     local = local % max(1, ndev)
@@ -134,56 +170,70 @@ def main():
         else:
             dist.init_process_group(backend)
     dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(v):
+        if world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def timed(fn, reps):
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize(dev)
+        barrier()
+        return max_over_ranks(time.perf_counter() - t0)
+
+    # ---------------- headline: 2^24 GF(2^128) additive NTT, one transform per rank
     log_h = a.log_h
     n = 1 << log_h
-
-    # synthetic input generated on the host, resident in HBM before timing
     x = np.random.default_rng(0xDEADBEEF + log_h + rank).integers(0, 2**32, size=4 * n, dtype=np.uint64)
     d_in = torch.from_numpy(x.astype(np.uint32).view(np.int32)).to(dev)
     del x
     d_out = torch.empty_like(d_in)
     ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(7), device=local))
-    stream = torch.cuda.current_stream(dev)
-
     for _ in range(a.warmup):
         ntt.forward_device(d_in, d_out, stream=stream)
     torch.cuda.synchronize(dev)
 
-    # per-kernel timing with hipEvents on the launch stream (separate, untimed pass)
-    ntt.set_event_timing(True)
-    for _ in range(max(3, min(a.steps, 10))):
-        ntt.forward_device(d_in, d_out, stream=stream)
-    kind_ms = ntt.event_timing()
-    ntt.set_event_timing(False)
+    # per-pass durations: each pass launched back to back on the launch stream between two
+    # hipEvents (steady-state duration per launch, as in the timed loop; bn_antt_time_passes)
+    scratch = torch.empty_like(d_out)
+    pass_ms = ntt.time_passes(d_in, scratch, reps=max(5, min(a.steps, 20)), stream=stream)
+    del scratch
     torch.cuda.synchronize(dev)
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        ntt.forward_device(d_in, d_out, stream=stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-
+    dt = timed(lambda: ntt.forward_device(d_in, d_out, stream=stream), a.steps)
     ms_step = dt / a.steps * 1e3
     elems_per_s = world * n / (dt / a.steps)
-    alg_bytes = 2 * 16 * n  # read input once + write output once (SURVEY.md §8d)
+    alg_bytes = 2 * 16 * n  # read input once + write output once (SURVEY.md section 8d)
     transform_gbps = alg_bytes / (ms_step * 1e-3) / 1e9
 
+    res = None
     if rank == 0:
-        # dominant kernel = the pass with the largest mean hipEvent duration; each pass reads and
-        # writes the whole vector once, so its algorithmic bytes are the same 32 B/element.
-        dom = max(range(len(kind_ms)), key=lambda i: kind_ms[i]) if kind_ms else None
-        dom_ms = kind_ms[dom] if dom is not None else ms_step
+        # dominant kernel = the pass with the largest mean duration; every pass reads and writes
+        # the whole vector once, so its algorithmic bytes are the same 32 B/element
+        dom = max(range(len(pass_ms)), key=lambda i: pass_ms[i]) if pass_ms else None
+        dom_ms = pass_ms[dom] if dom is not None else ms_step
         achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-        pmc = load_pmc(log_h)
+        ctr = load_pass_counters(log_h)
+        traffic = load_traffic(log_h)
+        valu = None
+        if ctr and dom is not None and str(dom) in ctr and ctr[str(dom)].get("SQ_INSTS_VALU"):
+            insts = ctr[str(dom)]["SQ_INSTS_VALU"]
+            rate = insts / (dom_ms * 1e-3)
+            valu = {"insts_per_launch": insts, "achieved": rate, "peak": VALU_PEAK_WAVE_INSTS,
+                    "unit": "wave64 instructions/s", "frac": rate / VALU_PEAK_WAVE_INSTS,
+                    "source": "profiles/r02/pmc_summary.json"}
         res = {
             "metric": "GF(2^128) additive-NTT elements/sec (2^24 pts)",
             "value": elems_per_s,
@@ -207,26 +257,130 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
-                "traffic": pmc,
-                "kernel": "pass %s of %d" % (dom, len(kind_ms)),
+                "traffic": traffic.get(str(dom)) if traffic and dom is not None else None,
+                "kernel": "pass %s of %d" % (dom, len(pass_ms)),
                 "kernel_ms": dom_ms,
-                "pass_ms": kind_ms,
+                "pass_ms": pass_ms,
                 "transform_frac": transform_gbps / HBM_PEAK_GBPS,
+                # the pass kernels are VALU-issue bound
+                "limiter": "valu-issue",
             },
-            # the pass kernels are VALU-issue bound: wave-instructions per launch
-            # (SQ_INSTS_VALU, committed PMC run) / the live hipEvent duration vs the issue peak of
-            # 256 CU x 4 SIMD x 0.5 wave64 instructions/cycle x 2.4 GHz
-            "valu": valu_block(dom, dom_ms),
+            "valu": valu,
         }
+    del d_in, d_out
+
+    # ---------------- config 5: 256 x 2^20 batched NTT, sharded by transform
+    c5 = None
+    if not a.no_c5:
+        c5 = {}
+        lo, hi = D.batch_slice(a.c5_batch, rank, world)
+        mine = hi - lo
+        nb = 1 << a.c5_log_n
+        bt_in = torch.randint(-2**31, 2**31 - 1, (max(mine, 1) * 4 * nb,), dtype=torch.int32, device=dev)
+        bt_out = torch.empty_like(bt_in)
+        bplan = B.AdditiveNTT(B.AdditiveNTTConf(a.c5_log_n, 0, B.FanPaarTowerField(7), device=local))
+
+        def run_batch():
+            if mine:
+                bplan.forward_device(bt_in, bt_out, batch=mine, stream=stream)
+
+        run_batch()
+        torch.cuda.synchronize(dev)
+        dtb = timed(run_batch, a.c5_steps) / a.c5_steps
+        c5["batched_ntt"] = {
+            "workload": "%d x 2^%d-point GF(2^128) additive NTT, %d per rank (rank-contiguous slices, no collective)"
+                        % (a.c5_batch, a.c5_log_n, -(-a.c5_batch // world)),
+            "ms": dtb * 1e3, "elements_per_s": a.c5_batch * nb / dtb,
+            "per_gpu_hbm_frac": (-(-a.c5_batch // world)) * 32 * nb / dtb / 1e9 / HBM_PEAK_GBPS,
+            "scaling": "strong", "steps": a.c5_steps}
+        del bt_in, bt_out, bplan
+        torch.cuda.empty_cache()
+
+        # ---------------- config 5: 2^28-eval d=3 sumcheck, sharded by 32-element batch
+        N, d = a.sc_log_n, a.sc_d
+        local_words = d * (4 << N) // world
+        chunks = []
+        left = local_words
+        while left:
+            m = min(left, 1 << 30)
+            chunks.append(torch.randint(-2**31, 2**31 - 1, (m,), dtype=torch.int32, device=dev))
+            left -= m
+        shard = torch.cat(chunks) if len(chunks) > 1 else chunks[0]
+        del chunks
+        rng = np.random.default_rng(0xC4A1)
+        challenges = rng.integers(0, 2**32, size=(N, 4), dtype=np.uint64).astype(np.uint32)
+        group = None
+
+        def run_sumcheck(check):
+            prover = B.Sumcheck.from_shard(N, d, shard, rank, world, device=local)
+            sc = D.ShardedSumcheck(prover, group)
+            barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            claim = None
+            ok = True
+            for i in range(N):
+                s, pts = sc.this_round_messages()
+                if check:
+                    if claim is not None and not np.array_equal(s, claim):
+                        ok = False
+                    if not np.array_equal(s, pts[0] ^ pts[1]):
+                        ok = False
+                    claim = B.evaluate_univariate_given_points(challenges[i], pts)
+                sc.move_to_next_round(challenges[i])
+            s, _ = sc.this_round_messages()  # final claim: prod_j f_j(r)
+            if check and claim is not None and not np.array_equal(s, claim):
+                ok = False
+            torch.cuda.synchronize(dev)
+            barrier()
+            el = max_over_ranks(time.perf_counter() - t0)
+            prover.close()
+            return el, ok
+
+        run_sumcheck(False)  # warm-up (kernels, allocator, collectives)
+        times, oks = [], []
+        for _ in range(max(1, a.sc_runs)):
+            el, ok = run_sumcheck(True)
+            times.append(el)
+            oks.append(ok)
+        tsc = sorted(times)[len(times) // 2]
+        alg = sum(d * 16 * ((1 << (N - i)) + (1 << (N - i - 1))) for i in range(N))
+        c5["sumcheck"] = {
+            "workload": "GF(2^128) sumcheck, 2^%d evals, d=%d, bitsliced, sharded %d ways by 32-element batch; "
+                        "all %d rounds incl. per-round all-gather+XOR of partial messages" % (N, d, world, N),
+            "ms": tsc * 1e3, "evals_per_s": (1 << N) / tsc, "runs": len(times),
+            "protocol_checks_pass": all(oks),
+            "per_gpu_alg_gbps": alg / world / tsc / 1e9,
+            "collective": "all_gather (%s) + XOR" % (backend if world > 1 else "none, world 1")}
+        del shard
+        torch.cuda.empty_cache()
+
+    if rank == 0:
+        res["c5"] = c5
         if world == 1:
-            res["apply_e2e"] = apply_e2e(B, ntt, d_in, n)
-        if not a.no_cpu and world == 1:
-            res["cpu_baseline"] = cpu_baseline(a.cpu_log_h)
-        else:
-            res["cpu_baseline"] = None
+            res["apply_e2e"] = apply_e2e(B, ntt, n)
+        res["cpu_baseline"] = cpu_baseline() if (not a.no_cpu and world == 1) else None
         print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()
+
+
+def apply_e2e(B, ntt, n, reps=3):
+    """Reference-semantics AdditiveNTT::apply (host buffers: H2D + transform + D2H, synchronous);
+    reported beside `value`, never as it (SURVEY.md section 8d)."""
+    import numpy as np
+    host = np.random.default_rng(7).integers(0, 2**32, size=(n, 4), dtype=np.uint64).astype(np.uint32)
+    inp = B.NTTData(n, B.DataOrder.IN_ORDER, 128, host)
+    out = B.NTTData(n, B.DataOrder.INVALID, 128)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        if not ntt.apply(inp, out):
+            return None
+        ts.append(time.perf_counter() - t0)
+    t = sorted(ts)[len(ts) // 2]
+    return {"ms": t * 1e3, "elements_per_s": n / t, "reps": reps,
+            "note": "AdditiveNTT.apply on pageable host buffers (PCIe-inclusive), median"}
 
 
 if __name__ == "__main__":

@@ -121,29 +121,49 @@ __global__ __launch_bounds__(256) void antt_v0_group(V0Params p) {
 }
 
 // Optional per-launch hipEvent timing (bench.py): events are recorded on the launch stream
-// around each kernel; `kind` identifies the pass.
+// around each kernel and resolved later (timing_resolve), so timing does not serialise the
+// passes; `kind` identifies the pass.
+static int timing_event(bn_antt_plan* p, hipEvent_t* e) {
+	if (!p->ev_pool.empty()) {
+		*e = p->ev_pool.back();
+		p->ev_pool.pop_back();
+		return BN_OK;
+	}
+	BN_HIP(hipEventCreate(e));
+	return BN_OK;
+}
 int timing_begin(bn_antt_plan* p, int kind, hipStream_t st) {
 	if (!p->timing) return BN_OK;
-	while ((int)p->ev.size() < 2 * (kind + 1)) {
-		hipEvent_t e;
-		BN_HIP(hipEventCreate(&e));
-		p->ev.push_back(e);
-	}
-	if ((int)p->kind_ms.size() < kind + 1) {
-		p->kind_ms.resize(kind + 1, 0.f);
-		p->kind_cnt.resize(kind + 1, 0);
-	}
-	BN_HIP(hipEventRecord(p->ev[2 * kind], st));
+	(void)kind;
+	int rc = timing_event(p, &p->cur_begin);
+	if (rc != BN_OK) return rc;
+	BN_HIP(hipEventRecord(p->cur_begin, st));
 	return BN_OK;
 }
 int timing_end(bn_antt_plan* p, int kind, hipStream_t st) {
 	if (!p->timing) return BN_OK;
-	BN_HIP(hipEventRecord(p->ev[2 * kind + 1], st));
-	BN_HIP(hipEventSynchronize(p->ev[2 * kind + 1]));
-	float ms = 0.f;
-	BN_HIP(hipEventElapsedTime(&ms, p->ev[2 * kind], p->ev[2 * kind + 1]));
-	p->kind_ms[kind] += ms;
-	p->kind_cnt[kind] += 1;
+	hipEvent_t e;
+	int rc = timing_event(p, &e);
+	if (rc != BN_OK) return rc;
+	BN_HIP(hipEventRecord(e, st));
+	p->pending.push_back({kind, p->cur_begin, e});
+	return BN_OK;
+}
+static int timing_resolve(bn_antt_plan* p) {
+	for (const auto& q : p->pending) {
+		BN_HIP(hipEventSynchronize(q.end));
+		float ms = 0.f;
+		BN_HIP(hipEventElapsedTime(&ms, q.begin, q.end));
+		if ((int)p->kind_ms.size() < q.kind + 1) {
+			p->kind_ms.resize(q.kind + 1, 0.f);
+			p->kind_cnt.resize(q.kind + 1, 0);
+		}
+		p->kind_ms[q.kind] += ms;
+		p->kind_cnt[q.kind] += 1;
+		p->ev_pool.push_back(q.begin);
+		p->ev_pool.push_back(q.end);
+	}
+	p->pending.clear();
 	return BN_OK;
 }
 
@@ -184,6 +204,8 @@ int launch_v0(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, hipStre
 int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st);
 bool bs_supports(const bn_antt_plan* plan);
 int bs_prepare(bn_antt_plan* plan);
+int bs_time_passes(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, int reps,
+                   hipStream_t st, float* ms, int max_passes, int* n_out);
 
 }  // namespace bn
 
@@ -243,7 +265,12 @@ extern "C" int bn_antt_plan_destroy(bn_antt_plan* p) {
 	if (p->scratch) hipFree(p->scratch);
 	if (p->h_dev_in) hipFree(p->h_dev_in);
 	if (p->h_dev_out) hipFree(p->h_dev_out);
-	for (auto e : p->ev) hipEventDestroy(e);
+	for (const auto& q : p->pending) {
+		hipEventSynchronize(q.end);
+		hipEventDestroy(q.begin);
+		hipEventDestroy(q.end);
+	}
+	for (auto e : p->ev_pool) hipEventDestroy(e);
 	if (p->own_stream) hipStreamDestroy(p->own_stream);
 	hipSetDevice(dev_prev);
 	delete p;
@@ -343,14 +370,33 @@ extern "C" int bn_antt_plan_set_variant(bn_antt_plan* p, int variant) {
 
 extern "C" int bn_antt_set_event_timing(bn_antt_plan* p, int enable) {
 	BN_CHECK_ARG(p != nullptr, "plan is NULL");
+	int rc = timing_resolve(p);  // drop what an earlier timing window left
+	if (rc != BN_OK) return rc;
 	p->timing = enable;
 	p->kind_ms.clear();
 	p->kind_cnt.clear();
 	return BN_OK;
 }
 
+extern "C" int bn_antt_time_passes(bn_antt_plan* p, const void* d_in, void* d_out, size_t batch, int reps,
+                                   void* stream, float* ms_per_pass, int max_passes, int* n_passes) {
+	BN_CHECK_ARG(p != nullptr && d_in != nullptr && d_out != nullptr && ms_per_pass != nullptr && n_passes != nullptr,
+	             "NULL argument");
+	BN_CHECK_ARG(batch >= 1 && reps >= 1, "batch and reps must be >= 1");
+	if (p->variant != 1) BN_FAIL(BN_ERR_UNSUPPORTED, "pass timing is built for kernel variant 1");
+	int dev_prev = 0;
+	hipGetDevice(&dev_prev);
+	if (dev_prev != p->device) BN_HIP(hipSetDevice(p->device));
+	const int rc = bs_time_passes(p, (const uint32_t*)d_in, (uint32_t*)d_out, batch, reps, (hipStream_t)stream,
+	                              ms_per_pass, max_passes, n_passes);
+	if (dev_prev != p->device) hipSetDevice(dev_prev);
+	return rc;
+}
+
 extern "C" int bn_antt_get_event_timing(bn_antt_plan* p, float* ms, int max_kinds, int* n_kinds) {
 	BN_CHECK_ARG(p != nullptr && n_kinds != nullptr, "NULL argument");
+	int rc = timing_resolve(p);
+	if (rc != BN_OK) return rc;
 	*n_kinds = (int)p->kind_ms.size();
 	for (int i = 0; i < *n_kinds && i < max_kinds; i++) ms[i] = p->kind_cnt[i] ? p->kind_ms[i] / p->kind_cnt[i] : 0.f;
 	return BN_OK;

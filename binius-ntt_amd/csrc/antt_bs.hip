@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 #include "antt_plan.hpp"
@@ -551,64 +552,130 @@ int bs_prepare(bn_antt_plan* plan) {
 	return BN_OK;
 }
 
-int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st) {
-	const auto passes = plan_passes(plan);
-	const int L = plan->limbs;
-	// debug hooks: BN_DEBUG_MAX_PASSES=n runs only the first n passes, BN_DEBUG_STOP_STAGE=s runs
-	// only stages >= s, BN_PF=1/2 enables next-tile prefetch for GF(2^8)-only / all passes, BN_PERSIST=0 launches
-	// one workgroup per tile, BN_TRACE=1 prints per-wave phase times (cycles)
-	size_t npass = passes.size();
-	if (const char* e = getenv("BN_DEBUG_MAX_PASSES")) npass = std::min(npass, (size_t)atoi(e));
-	int pf_mode = 0;
-	if (const char* e = getenv("BN_PF")) pf_mode = atoi(e);
-	bool persist = true;
-	if (const char* e = getenv("BN_PERSIST")) persist = atoi(e) != 0;
-	for (size_t i = 0; i < npass; i++) {
-		BsParams prm;
-		prm.src = d_in;
-		prm.dst = d_out;
-		prm.log_h = plan->log_h;
-		prm.log_rate = plan->log_rate;
-		prm.dbg = 0;
-		if (const char* e = getenv("BN_DEBUG_FLAGS")) prm.dbg = atoi(e);
-		prm.p = passes[i];
-		prm.p.stop_j = 0;
-		if (const char* e = getenv("BN_DEBUG_STOP_STAGE"))
-			prm.p.stop_j = std::max(0, std::min(prm.p.k, atoi(e) - prm.p.lo));
-		const size_t ntiles = (batch << plan->log_rate) << passes[i].n_outer;
-		// two 74-KB tiles per CU: a persistent grid of two workgroups per CU walks all tiles
-		const int fmax = pass_fmax(passes[i]);
-		const bool pf = persist && (pf_mode == 2 || (pf_mode == 1 && fmax <= 8));
-		const size_t grid = pf ? std::min(ntiles, (size_t)2 * (size_t)plan->num_cus) : ntiles;
-		prm.ntiles = ntiles;
-		prm.trace = nullptr;
-		static unsigned long long* trbuf = nullptr;
-		if (getenv("BN_TRACE")) {
-			if (!trbuf) BN_HIP(hipMalloc(&trbuf, (size_t)1 << 26));
-			BN_HIP(hipMemset(trbuf, 0, grid * L * 8 * 8));
-			prm.trace = trbuf;
-		}
-		int rc = timing_begin(plan, (int)i, st);
-		if (rc != BN_OK) return rc;
-		void* args[] = {&prm};
-		BN_HIP(hipLaunchKernel(kernel_for(L, passes[i].role, fmax, pf), dim3((unsigned)grid), dim3(64 * L), args,
-		                       lds_bytes(L), st));
-		rc = timing_end(plan, (int)i, st);
-		if (rc != BN_OK) return rc;
-		if (prm.trace) {
-			const size_t g = grid * (size_t)L;
-			std::vector<unsigned long long> h(g * 8);
-			BN_HIP(hipStreamSynchronize(st));
-			BN_HIP(hipMemcpy(h.data(), prm.trace, g * 8 * 8, hipMemcpyDeviceToHost));
-			double acc[8] = {0};
-			for (size_t w = 0; w < g; w++)
-				for (int k = 0; k < 8; k++) acc[k] += (double)h[w * 8 + k];
-			const double t = acc[4] > 0 ? acc[4] : 1;  // wave-tiles
-			fprintf(stderr,
-			        "trace pass %zu (fmax %d pf %d, %zu wave-tiles, cycles per wave-tile): load %.0f  block %.0f [pre %.0f mul %.0f post %.0f]  inword+tr %.0f  store %.0f\n",
-			        i, fmax, (int)pf, (size_t)acc[4], acc[0] / t, acc[1] / t, acc[5] / t, acc[6] / t, acc[7] / t, acc[2] / t, acc[3] / t);
-		}
+static const BsPass* bs_passes(bn_antt_plan* plan, size_t* n_passes) {
+	// the pass tables depend only on the plan: built once and cached in it
+	if (plan->bs_passes.empty()) {
+		const auto ps = plan_passes(plan);
+		plan->bs_passes.resize(ps.size() * sizeof(BsPass));
+		memcpy(plan->bs_passes.data(), ps.data(), plan->bs_passes.size());
 	}
+	*n_passes = plan->bs_passes.size() / sizeof(BsPass);
+	return (const BsPass*)plan->bs_passes.data();
+}
+
+struct BsDevKnobs {
+	int pf_mode = 0, dbg = 0, stop_stage = -1;
+	bool persist = true, trace = false;
+	size_t max_passes = ~(size_t)0;
+};
+
+static BsDevKnobs dev_knobs() {
+	BsDevKnobs k;
+#ifdef BN_DEV
+	// development build only (make BN_DEV=1): BN_DEBUG_MAX_PASSES=n runs only the first n passes,
+	// BN_DEBUG_STOP_STAGE=s runs only stages >= s, BN_DEBUG_FLAGS skips work (see BsParams::dbg),
+	// BN_PF=1/2 enables next-tile prefetch for GF(2^8)-only / all passes, BN_PERSIST=0 launches
+	// one workgroup per tile, BN_TRACE=1 prints per-wave phase times (cycles)
+	if (const char* e = getenv("BN_DEBUG_MAX_PASSES")) k.max_passes = (size_t)atoi(e);
+	if (const char* e = getenv("BN_PF")) k.pf_mode = atoi(e);
+	if (const char* e = getenv("BN_PERSIST")) k.persist = atoi(e) != 0;
+	if (const char* e = getenv("BN_DEBUG_FLAGS")) k.dbg = atoi(e);
+	if (const char* e = getenv("BN_DEBUG_STOP_STAGE")) k.stop_stage = atoi(e);
+	k.trace = getenv("BN_TRACE") != nullptr;
+#endif
+	return k;
+}
+
+// one launch of pass i of the transform
+static int launch_one(bn_antt_plan* plan, const BsPass& pass, int i, const uint32_t* d_in, uint32_t* d_out,
+                      size_t batch, hipStream_t st, const BsDevKnobs& kn) {
+	const int L = plan->limbs;
+	BsParams prm;
+	prm.src = d_in;
+	prm.dst = d_out;
+	prm.log_h = plan->log_h;
+	prm.log_rate = plan->log_rate;
+	prm.dbg = kn.dbg;
+	prm.p = pass;
+	prm.p.stop_j = kn.stop_stage < 0 ? 0 : std::max(0, std::min(prm.p.k, kn.stop_stage - prm.p.lo));
+	const size_t ntiles = (batch << plan->log_rate) << pass.n_outer;
+	// two 74-KB tiles per CU: a persistent grid of two workgroups per CU walks all tiles
+	const int fmax = pass_fmax(pass);
+	const bool pf = kn.persist && (kn.pf_mode == 2 || (kn.pf_mode == 1 && fmax <= 8));
+	const size_t grid = pf ? std::min(ntiles, (size_t)2 * (size_t)plan->num_cus) : ntiles;
+	prm.ntiles = ntiles;
+	prm.trace = nullptr;
+	static unsigned long long* trbuf = nullptr;
+	if (kn.trace) {
+		if (!trbuf) BN_HIP(hipMalloc(&trbuf, (size_t)1 << 26));
+		BN_HIP(hipMemset(trbuf, 0, grid * L * 8 * 8));
+		prm.trace = trbuf;
+	}
+	int rc = timing_begin(plan, i, st);
+	if (rc != BN_OK) return rc;
+	void* args[] = {&prm};
+	BN_HIP(hipLaunchKernel(kernel_for(L, pass.role, fmax, pf), dim3((unsigned)grid), dim3(64 * L), args, lds_bytes(L), st));
+	rc = timing_end(plan, i, st);
+	if (rc != BN_OK) return rc;
+	if (prm.trace) {
+		const size_t g = grid * (size_t)L;
+		std::vector<unsigned long long> h(g * 8);
+		BN_HIP(hipStreamSynchronize(st));
+		BN_HIP(hipMemcpy(h.data(), prm.trace, g * 8 * 8, hipMemcpyDeviceToHost));
+		double acc[8] = {0};
+		for (size_t w = 0; w < g; w++)
+			for (int k = 0; k < 8; k++) acc[k] += (double)h[w * 8 + k];
+		const double t = acc[4] > 0 ? acc[4] : 1;  // wave-tiles
+		fprintf(stderr,
+		        "trace pass %d (fmax %d pf %d, %zu wave-tiles, cycles per wave-tile): load %.0f  block %.0f [pre %.0f mul %.0f post %.0f]  inword+tr %.0f  store %.0f\n",
+		        i, fmax, (int)pf, (size_t)acc[4], acc[0] / t, acc[1] / t, acc[5] / t, acc[6] / t, acc[7] / t, acc[2] / t, acc[3] / t);
+	}
+	return BN_OK;
+}
+
+int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st) {
+	size_t n_passes = 0;
+	const BsPass* passes = bs_passes(plan, &n_passes);
+	const BsDevKnobs kn = dev_knobs();
+	const size_t npass = std::min(n_passes, kn.max_passes);
+	for (size_t i = 0; i < npass; i++) {
+		int rc = launch_one(plan, passes[i], (int)i, d_in, d_out, batch, st, kn);
+		if (rc != BN_OK) return rc;
+	}
+	return BN_OK;
+}
+
+// Profiling: each pass launched `reps` times back to back between two hipEvents on `st`
+// (steady-state duration per launch, no event between launches). The output buffer holds
+// no meaningful values afterwards (passes are re-applied to their own output); the cost of a
+// pass does not depend on the values (bitwise arithmetic, no data-dependent control flow).
+int bs_time_passes(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, int reps,
+                   hipStream_t st, float* ms, int max_passes, int* n_out) {
+	size_t n_passes = 0;
+	const BsPass* passes = bs_passes(plan, &n_passes);
+	BsDevKnobs kn = dev_knobs();
+	kn.trace = false;
+	const int saved = plan->timing;
+	plan->timing = 0;
+	hipEvent_t e0 = nullptr, e1 = nullptr;
+	int rc = BN_OK;
+	if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) rc = BN_ERR_HIP;
+	for (size_t i = 0; rc == BN_OK && i < n_passes; i++) {
+		// one untimed launch first: the pass's input is then the steady-state layout
+		rc = launch_one(plan, passes[i], (int)i, d_in, d_out, batch, st, kn);
+		if (rc == BN_OK && hipEventRecord(e0, st) != hipSuccess) rc = BN_ERR_HIP;
+		for (int r = 0; rc == BN_OK && r < reps; r++) rc = launch_one(plan, passes[i], (int)i, d_in, d_out, batch, st, kn);
+		if (rc == BN_OK && hipEventRecord(e1, st) != hipSuccess) rc = BN_ERR_HIP;
+		float t = 0.f;
+		if (rc == BN_OK && (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&t, e0, e1) != hipSuccess))
+			rc = BN_ERR_HIP;
+		if (rc == BN_OK && (int)i < max_passes) ms[i] = t / (float)reps;
+	}
+	if (e0) (void)hipEventDestroy(e0);
+	if (e1) (void)hipEventDestroy(e1);
+	plan->timing = saved;
+	if (rc != BN_OK) BN_FAIL(rc, "timing the passes failed");
+	*n_out = (int)n_passes;
 	return BN_OK;
 }
 

@@ -21,13 +21,21 @@ struct bn_antt_plan {
 	uint32_t* s_dev = nullptr;     // same on the device
 	uint32_t* scratch = nullptr;   // pass-intermediate buffer (variant-specific)
 	size_t scratch_bytes = 0;
+	std::vector<unsigned char> bs_passes;  // variant-1 pass tables (antt_bs.hip), built on first use
 	hipStream_t own_stream = nullptr;
 	// host-apply staging
 	void* h_dev_in = nullptr;
 	void* h_dev_out = nullptr;
-	// optional per-launch event timing
+	// optional per-launch event timing: events are recorded around each pass without any host
+	// synchronisation (the passes stay back to back) and resolved by bn_antt_get_event_timing
 	int timing = 0;
-	std::vector<hipEvent_t> ev;
+	struct PendingPass {
+		int kind;
+		hipEvent_t begin, end;
+	};
+	std::vector<hipEvent_t> ev_pool;
+	std::vector<PendingPass> pending;
+	hipEvent_t cur_begin = nullptr;
 	std::vector<float> kind_ms;
 	std::vector<int> kind_cnt;
 };

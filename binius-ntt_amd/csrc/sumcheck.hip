@@ -516,6 +516,53 @@ extern "C" int bn_sumcheck_create_device(int device, int num_vars, int d, int tr
 	return BN_OK;
 }
 
+// A shard prover built straight from this rank's share of bitsliced columns (the batches b with
+// b mod world == rank, in order: 4 * 2^num_vars / world words per column, columns back to back),
+// so no rank ever holds the whole input. The copy is ordered after the work queued on `stream`
+// (the caller's producer stream; NULL = the legacy default stream).
+extern "C" int bn_sumcheck_create_shard_device(int device, int num_vars, int d, int rank, int world,
+                                               const void* d_local, void* stream, bn_sumcheck** out) {
+	BN_CHECK_ARG(out, "NULL output pointer");
+	*out = nullptr;
+	BN_CHECK_ARG(d_local, "NULL evals");
+	int rc = check_shape(num_vars, d, 1);
+	if (rc != BN_OK) return rc;
+	BN_CHECK_ARG(world >= 1 && (world & (world - 1)) == 0, "world must be a power of two");
+	BN_CHECK_ARG(rank >= 0 && rank < world, "rank out of range");
+	const size_t n = (size_t)1 << num_vars;
+	BN_CHECK_ARG(n >= (size_t)32 * world, "need at least one 32-element batch per rank");
+	DeviceScope ds(device);
+	if (!ds.ok) BN_FAIL(BN_ERR_HIP, "hipSetDevice(%d) failed", device);
+	bn_sumcheck* sc = new bn_sumcheck;
+	sc->device = device;
+	sc->num_vars = num_vars;
+	sc->d = d;
+	const size_t col_words = 4 * n / (size_t)world;
+	if ((rc = sc_common_init(sc)) != BN_OK || (rc = sc_alloc(sc, col_words)) != BN_OK) {
+		sc_free(sc);
+		return rc;
+	}
+	hipEvent_t ready = nullptr;
+	hipError_t e = hipEventCreateWithFlags(&ready, hipEventDisableTiming);
+	if (e == hipSuccess) e = hipEventRecord(ready, (hipStream_t)stream);
+	if (e == hipSuccess) e = hipStreamWaitEvent(sc->stream, ready, 0);
+	if (e == hipSuccess)
+		e = hipMemcpyAsync(sc->cols, d_local, sizeof(uint32_t) * col_words * (size_t)d, hipMemcpyDeviceToDevice, sc->stream);
+	if (e == hipSuccess) e = hipStreamSynchronize(sc->stream);
+	if (ready) (void)hipEventDestroy(ready);
+	if (e != hipSuccess) {
+		sc_free(sc);
+		BN_FAIL(BN_ERR_HIP, "copying the shard: %s", hipGetErrorString(e));
+	}
+	sc->cur = n / (size_t)world;
+	sc->round = 0;
+	sc->rank = rank;
+	sc->world = world;
+	sc->sharded_used = world > 1;
+	*out = sc;
+	return BN_OK;
+}
+
 extern "C" int bn_sumcheck_set_shard(bn_sumcheck* sc, int rank, int world) {
 	BN_CHECK_ARG(sc, "NULL prover");
 	BN_CHECK_ARG(sc->round == 0 && !sc->sharded_used, "set_shard must precede the first round");

@@ -66,6 +66,7 @@ def lib():
         "bn_antt_plan_set_variant": (i32, [vp, i32]),
         "bn_antt_set_event_timing": (i32, [vp, i32]),
         "bn_antt_get_event_timing": (i32, [vp, ctypes.POINTER(ctypes.c_float), i32, ctypes.POINTER(i32)]),
+        "bn_antt_time_passes": (i32, [vp, vp, vp, sz, i32, vp, ctypes.POINTER(ctypes.c_float), i32, ctypes.POINTER(i32)]),
         "bn_gf128_mul_device": (i32, [vp, vp, vp, sz, vp]),
         "bn_gf128_mul_bitsliced_device": (i32, [vp, vp, vp, sz, vp]),
         "bn_gf32_mul_device": (i32, [vp, vp, vp, sz, vp]),
@@ -77,6 +78,7 @@ def lib():
         "bn_sumcheck_move_to_next_round": (i32, [vp, u32p]),
         "bn_sumcheck_round": (i32, [vp, ctypes.POINTER(i32)]),
         "bn_sumcheck_set_shard": (i32, [vp, i32, i32]),
+        "bn_sumcheck_create_shard_device": (i32, [i32, i32, i32, i32, i32, vp, vp, ctypes.POINTER(vp)]),
         "bn_sumcheck_needs_gather": (i32, [vp, ctypes.POINTER(i32)]),
         "bn_sumcheck_export_shard": (i32, [vp, u32p, sz]),
         "bn_sumcheck_import_gathered": (i32, [vp, u32p, sz, i32]),
@@ -119,6 +121,19 @@ def check_gpu_capabilities():
     return bool(lib().bn_check_gpu_capabilities())
 
 
+def _check_device_tensor(t, words, what):
+    """Shape/device/contiguity check before handing a raw pointer to the C-ABI: a short or
+    strided tensor would otherwise mean out-of-bounds device accesses."""
+    if isinstance(t, int):
+        return
+    if not t.is_cuda:
+        raise ValueError("%s must be a device tensor" % what)
+    if not t.is_contiguous():
+        raise ValueError("%s must be contiguous" % what)
+    if t.element_size() * t.numel() < 4 * words:
+        raise ValueError("%s holds %d bytes, need %d" % (what, t.element_size() * t.numel(), 4 * words))
+
+
 def _ptr(t):
     """Device pointer of a torch tensor (or an int address)."""
     if isinstance(t, int):
@@ -126,10 +141,13 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
-def _stream(stream):
+def _stream(stream, device=None):
+    """hipStream_t for a launch: `stream` (torch stream or raw handle) or, when None, torch's
+    current stream of `device` (the plan's device, not whichever device is current)."""
     if stream is None:
         import torch
-        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        dev = torch.device("cuda", device) if device is not None else None
+        return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     if isinstance(stream, int):
         return ctypes.c_void_p(stream)
     return ctypes.c_void_p(stream.cuda_stream)
@@ -229,8 +247,13 @@ class AdditiveNTT:
         return True
 
     def forward_device(self, d_in, d_out, batch=1, stream=None):
-        """Device-resident transform(s) on torch tensors (or raw addresses); async on `stream`."""
-        _check(lib().bn_antt_forward_device(self._plan, _ptr(d_in), _ptr(d_out), batch, _stream(stream)))
+        """Device-resident transform(s) on torch tensors (or raw addresses); async on `stream`
+        (default: torch's current stream of the plan's device)."""
+        n = (1 << self.conf.log_h) * self.limbs * batch
+        _check_device_tensor(d_in, n, "d_in")
+        _check_device_tensor(d_out, n << self.conf.log_rate, "d_out")
+        _check(lib().bn_antt_forward_device(self._plan, _ptr(d_in), _ptr(d_out), batch,
+                                            _stream(stream, self.conf.device)))
 
     def subspace_evals(self):
         lh, w = self.conf.log_h, self.conf.log_h + self.conf.log_rate - 1
@@ -249,6 +272,17 @@ class AdditiveNTT:
 
     def set_event_timing(self, enable):
         _check(lib().bn_antt_set_event_timing(self._plan, 1 if enable else 0))
+
+    def time_passes(self, d_in, d_out, reps=10, batch=1, stream=None):
+        """Steady-state ms per launch of each pass (bn_antt_time_passes); d_out is scratch."""
+        n = (1 << self.conf.log_h) * self.limbs * batch
+        _check_device_tensor(d_in, n, "d_in")
+        _check_device_tensor(d_out, n << self.conf.log_rate, "d_out")
+        arr = (ctypes.c_float * 16)()
+        k = ctypes.c_int()
+        _check(lib().bn_antt_time_passes(self._plan, _ptr(d_in), _ptr(d_out), batch, reps,
+                                         _stream(stream, self.conf.device), arr, 16, ctypes.byref(k)))
+        return [arr[i] for i in range(min(k.value, 16))]
 
     def event_timing(self):
         arr = (ctypes.c_float * 16)()
@@ -344,28 +378,51 @@ class NTT:
 
     def forward_device(self, d_in, d_out, batch=1, bit_reversed=False, stream=None):
         _check(lib().bn_bb31_ntt_forward_device(self._plan, _ptr(d_in), _ptr(d_out), batch,
-                                                1 if bit_reversed else 0, _stream(stream)))
+                                                1 if bit_reversed else 0, _stream(stream, self.conf.device)))
 
 
 # ------------------------------------------------------------------ field / bitslicing
+def _dev_index(t):
+    return None if isinstance(t, int) else t.device.index
+
+
+def _same_size(what, *ts):
+    sizes = {t.numel() * t.element_size() for t in ts if not isinstance(t, int)}
+    if len(sizes) > 1:
+        raise ValueError("%s operands differ in size: %s" % (what, sorted(sizes)))
+
+
 def gf128_mul(a, b, out, stream=None):
-    _check(lib().bn_gf128_mul_device(_ptr(a), _ptr(b), _ptr(out), a.numel() // 4, _stream(stream)))
+    _same_size("gf128_mul", a, b, out)
+    for t, w in ((a, "a"), (b, "b"), (out, "out")):
+        _check_device_tensor(t, a.numel(), w)
+    _check(lib().bn_gf128_mul_device(_ptr(a), _ptr(b), _ptr(out), a.numel() // 4, _stream(stream, _dev_index(a))))
 
 
 def gf32_mul(a, b, out, stream=None):
-    _check(lib().bn_gf32_mul_device(_ptr(a), _ptr(b), _ptr(out), a.numel(), _stream(stream)))
+    _same_size("gf32_mul", a, b, out)
+    for t, w in ((a, "a"), (b, "b"), (out, "out")):
+        _check_device_tensor(t, a.numel(), w)
+    _check(lib().bn_gf32_mul_device(_ptr(a), _ptr(b), _ptr(out), a.numel(), _stream(stream, _dev_index(a))))
 
 
 def gf128_mul_bitsliced(a, b, out, stream=None):
-    _check(lib().bn_gf128_mul_bitsliced_device(_ptr(a), _ptr(b), _ptr(out), a.numel() // 128, _stream(stream)))
+    _same_size("gf128_mul_bitsliced", a, b, out)
+    for t, w in ((a, "a"), (b, "b"), (out, "out")):
+        _check_device_tensor(t, a.numel(), w)
+    _check(lib().bn_gf128_mul_bitsliced_device(_ptr(a), _ptr(b), _ptr(out), a.numel() // 128,
+                                               _stream(stream, _dev_index(a))))
 
 
 def gf128_mul_repeat(kind, state, operand, threads, iters, stream=None):
-    _check(lib().bn_gf128_mul_repeat_device(kind, _ptr(state), _ptr(operand), threads, iters, _stream(stream)))
+    _check(lib().bn_gf128_mul_repeat_device(kind, _ptr(state), _ptr(operand), threads, iters,
+                                            _stream(stream, _dev_index(state))))
 
 
 def bitslice(buf, untranspose=False, stream=None):
-    _check(lib().bn_bitslice_device(_ptr(buf), buf.numel() // 128, 1 if untranspose else 0, _stream(stream)))
+    _check_device_tensor(buf, buf.numel(), "buf")
+    _check(lib().bn_bitslice_device(_ptr(buf), buf.numel() // 128, 1 if untranspose else 0,
+                                    _stream(stream, _dev_index(buf))))
 
 
 # ------------------------------------------------------------------ sumcheck
@@ -380,11 +437,30 @@ class Sumcheck:
             _check(lib().bn_sumcheck_create(device, num_vars, composition_size, 1 if data_is_transposed else 0,
                                             ev.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(p)))
         else:
+            _check_device_tensor(evals, composition_size * 4 << num_vars, "evals")
+            # the library copies on its own stream: the producer (an NTT, a torch kernel) must be done
+            import torch
+            torch.cuda.current_stream(evals.device).synchronize()
             _check(lib().bn_sumcheck_create_device(device, num_vars, composition_size,
                                                    1 if data_is_transposed else 0, _ptr(evals), 0, ctypes.byref(p)))
         self._sc = p
         if shard is not None:
             _check(lib().bn_sumcheck_set_shard(self._sc, shard[0], shard[1]))
+
+    @classmethod
+    def from_shard(cls, num_vars, composition_size, local_evals, rank, world, device=0, stream=None):
+        """Shard prover from this rank's share only (bn_sumcheck_create_shard_device): local_evals
+        is a device tensor of composition_size * 4 * 2^num_vars / world words (bitsliced batches
+        b with b mod world == rank, in order); the copy is ordered after `stream`."""
+        _check_device_tensor(local_evals, composition_size * (4 << num_vars) // world, "local_evals")
+        self = cls.__new__(cls)
+        self.num_vars, self.d = num_vars, composition_size
+        p = ctypes.c_void_p()
+        _check(lib().bn_sumcheck_create_shard_device(device, num_vars, composition_size, rank, world,
+                                                     _ptr(local_evals), _stream(stream, local_evals.device.index),
+                                                     ctypes.byref(p)))
+        self._sc = p
+        return self
 
     def this_round_messages(self):
         s = np.zeros(4, np.uint32)

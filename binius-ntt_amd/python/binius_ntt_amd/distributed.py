@@ -59,7 +59,7 @@ class ShardedSumcheck:
         import torch.distributed as dist
         self.prover = prover
         self.group = group
-        self.world = dist.get_world_size(group)
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.replicated = self.world == 1  # after the endgame gather every rank holds everything
 
     def _gather_if_needed(self):

@@ -85,6 +85,13 @@ int bn_antt_plan_set_variant(bn_antt_plan* plan, int variant);
  * bn_antt_forward_device call on its stream and returns per-launch-kind mean durations. */
 int bn_antt_set_event_timing(bn_antt_plan* plan, int enable);
 int bn_antt_get_event_timing(bn_antt_plan* plan, float* ms_per_kind, int max_kinds, int* n_kinds);
+/* Profiling (no reference counterpart; bench.py's roofline): every pass of the transform is
+ * launched `reps` times back to back on `stream` between two hipEvents, giving its steady-state
+ * duration per launch in ms_per_pass[pass]. d_out's contents are meaningless afterwards (passes
+ * are re-applied to their own output; their cost does not depend on the values). Variant 1
+ * only. Synchronous. */
+int bn_antt_time_passes(bn_antt_plan* plan, const void* d_in, void* d_out, size_t batch, int reps,
+                        void* stream, float* ms_per_pass, int max_passes, int* n_passes);
 
 /* ------------------------------------------------------------------------------------
  * Binary tower field arithmetic (src/ulvt/finite_fields/)
@@ -127,7 +134,10 @@ int bn_sumcheck_create(int device, int num_vars, int composition_size, int data_
                        const uint32_t* evals, bn_sumcheck** sc);
 /* As above but from device memory already holding the columns (no host copy). The buffer
  * is copied into the prover's own storage unless take_ownership != 0, in which case the
- * prover folds it in place and frees it with hipFree on destroy. */
+ * prover folds it in place and frees it with hipFree on destroy (so it must come from
+ * hipMalloc). Precondition: the columns are complete when this is called (the copy runs on
+ * the prover's own stream, unordered with the caller's streams); the Python mirror
+ * synchronises the current stream first. */
 int bn_sumcheck_create_device(int device, int num_vars, int composition_size, int data_is_transposed,
                               void* d_evals, int take_ownership, bn_sumcheck** sc);
 /* Replaces Sumcheck::this_round_messages(sum, points) (sumcheck.cuh:130-246):
@@ -142,6 +152,13 @@ int bn_sumcheck_round(const bn_sumcheck* sc, int* round);
  * the caller (the Python/RCCL layer does allgather + XOR). world must be a power of two
  * with 32*world <= 2^num_vars. Must be called before the first round. */
 int bn_sumcheck_set_shard(bn_sumcheck* sc, int rank, int world);
+/* A shard prover built directly from this rank's share (no reference counterpart): d_local
+ * holds the bitsliced batches b with b mod world == rank, in order (4*2^num_vars/world words per
+ * column, columns back to back). The copy is ordered after the work queued on `stream` (a
+ * hipStream_t; NULL = default stream). Equivalent to bn_sumcheck_create_device on the whole
+ * input followed by bn_sumcheck_set_shard(rank, world), without any rank holding the whole. */
+int bn_sumcheck_create_shard_device(int device, int num_vars, int composition_size, int rank, int world,
+                                    const void* d_local, void* stream, bn_sumcheck** sc);
 /* Sharded endgame (no reference counterpart; the reference's analogue is the hand-over to the
  * CPU at 32 evaluations, sumcheck.cuh:283-297): once every shard is down to one 32-element
  * batch (*flag = 1), folds pair elements of different ranks. Each rank exports its batch
@@ -195,7 +212,9 @@ int bn_bb31_ntt_forward_host(bn_bb31_ntt_plan* plan, const uint32_t* in, size_t 
                              int in_bit_reversed);
 
 /* Device-resident, asynchronous on `stream` (hipStream_t, NULL = default): batch transforms of
- * 2^log_n words each, contiguous; d_in and d_out must not overlap. */
+ * 2^log_n words each, contiguous; d_in and d_out must not overlap. Multi-pass sizes
+ * (log_n >= 14) stage their data in the plan's scratch buffer, so a plan is used by one stream
+ * at a time (and not concurrently with forward_host); use one plan per stream. */
 int bn_bb31_ntt_forward_device(bn_bb31_ntt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch,
                                int in_bit_reversed, void* stream);
 

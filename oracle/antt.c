@@ -12,6 +12,8 @@
  * independent butterflies run; the serial loop below computes the same values (pinned by
  * the reference's MD5 table, test_ntt.cu:52-124).
  */
+#define _POSIX_C_SOURCE 200809L
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -180,4 +182,71 @@ void orc_antt128_limbwise_batch(const uint32_t* in, uint32_t* out, int log_h, in
 
 void orc_antt128_limbwise(const uint32_t* in, uint32_t* out, int log_h, int log_rate) {
 	orc_antt128_limbwise_batch(in, out, log_h, log_rate, 1);
+}
+
+/*
+ * All-cores CPU baseline (bench.py cpu_baseline): the same serial algorithm as
+ * orc_antt128_limbwise, with the butterflies of each stage split into contiguous ranges over
+ * `nthreads` pthreads (a barrier between stages, as the reference's kernel launches are).
+ * Flattened butterfly t of a stage: blk = t >> stage, k = t & (2^stage - 1).
+ */
+typedef struct {
+	const uint32_t* s;
+	uint32_t* d;
+	int width, log_h, log_rate, coset, nthreads, id;
+	pthread_barrier_t* bar;
+} mt_arg;
+
+static void* mt_worker(void* p) {
+	mt_arg* a = (mt_arg*)p;
+	const size_t n = (size_t)1 << a->log_h;
+	const size_t nbf = n / 2;
+	const size_t lo = nbf * (size_t)a->id / (size_t)a->nthreads, hi = nbf * (size_t)(a->id + 1) / (size_t)a->nthreads;
+	for (int stage = a->log_h - 1; stage >= 0; stage--) {
+		const size_t half = (size_t)1 << stage;
+		size_t cur_blk = (size_t)-1;
+		uint32_t w = 0;
+		for (size_t t = lo; t < hi; t++) {
+			const size_t blk = t >> stage, k = t & (half - 1);
+			if (blk != cur_blk) {
+				cur_blk = blk;
+				w = twiddle32(a->s, a->width, a->log_h, a->log_rate, a->coset, stage, blk);
+			}
+			uint32_t* u = a->d + 4 * ((blk << (stage + 1)) + k);
+			uint32_t* v = u + 4 * half;
+			for (int q = 0; q < 4; q++) {
+				u[q] ^= orc_mul32(w, v[q]);
+				v[q] ^= u[q];
+			}
+		}
+		pthread_barrier_wait(a->bar);
+	}
+	return NULL;
+}
+
+void orc_antt128_limbwise_mt(const uint32_t* in, uint32_t* out, int log_h, int log_rate, int nthreads) {
+	orc_init();
+	if (nthreads < 1) nthreads = 1;
+	const int width = log_h + log_rate - 1;
+	uint32_t* s = (uint32_t*)calloc((size_t)log_h * (size_t)(width > 0 ? width : 1), sizeof(uint32_t));
+	orc_subspace_evals32(log_h, log_rate, s);
+	const size_t n = (size_t)1 << log_h;
+	if ((size_t)nthreads > n / 2) nthreads = (int)(n / 2 > 0 ? n / 2 : 1);
+	pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+	mt_arg* args = (mt_arg*)calloc((size_t)nthreads, sizeof(mt_arg));
+	pthread_barrier_t bar;
+	for (int c = 0; c < (1 << log_rate); c++) {
+		uint32_t* d = out + 4 * (size_t)c * n;
+		memcpy(d, in, 4 * n * sizeof(uint32_t));
+		pthread_barrier_init(&bar, NULL, (unsigned)nthreads);
+		for (int i = 0; i < nthreads; i++) {
+			args[i] = (mt_arg){s, d, width, log_h, log_rate, c, nthreads, i, &bar};
+			pthread_create(&th[i], NULL, mt_worker, &args[i]);
+		}
+		for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+		pthread_barrier_destroy(&bar);
+	}
+	free(args);
+	free(th);
+	free(s);
 }

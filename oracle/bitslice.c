@@ -39,3 +39,13 @@ void orc_bitslice_untranspose128(uint32_t blk[128]) {
 	for (int c = 0; c < 4; c++) transpose32(tmp + 32 * c);
 	for (int i = 0; i < 128; i++) blk[4 * (i % 32) + i / 32] = tmp[i];
 }
+
+/* Bulk forms (test fixtures at large sizes): n_blocks consecutive 128-word blocks. */
+void orc_bitslice_many128(uint32_t* blocks, size_t n_blocks, int untranspose) {
+	for (size_t b = 0; b < n_blocks; b++) {
+		if (untranspose)
+			orc_bitslice_untranspose128(blocks + 128 * b);
+		else
+			orc_bitslice_transpose128(blocks + 128 * b);
+	}
+}

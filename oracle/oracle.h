@@ -63,6 +63,7 @@ void orc_antt128_limbwise(const uint32_t* in, uint32_t* out, int log_h, int log_
 /* Batched variant used by the CPU baseline: `batch` independent transforms,
  * element stride 4 words, transform stride 4 << log_h words.                  */
 void orc_antt128_limbwise_batch(const uint32_t* in, uint32_t* out, int log_h, int log_rate, int batch);
+void orc_antt128_limbwise_mt(const uint32_t* in, uint32_t* out, int log_h, int log_rate, int nthreads);
 
 /* ---------------- bitslicing (src/ulvt/utils/bitslicing.cuh:32-74) ---------------- */
 void orc_bitslice_transpose128(uint32_t blk[128]);
@@ -82,6 +83,9 @@ void orc_sumcheck_run(const uint32_t* evals, int n, int d, int bitsliced,
 /* evaluate_univariate_given_points (src/ulvt/sumcheck/test/verifier.cu:9-31)   */
 void orc_sumcheck_interpolate(const uint32_t* points, int num_points, const uint32_t challenge[4], uint32_t out[4]);
 /* evaluate_multilinear_composition (verifier.cu:88-107) on compact columns.     */
+void orc_multilinear_composition_fold_mt(const uint32_t* evals, int n, int d, int bitsliced, const uint32_t* challenges,
+                                         uint32_t out[4], int nthreads);
+void orc_bitslice_many128(uint32_t* blocks, size_t n_blocks, int untranspose);
 void orc_multilinear_composition(const uint32_t* evals_compact, int n, int d, const uint32_t* challenges, uint32_t out[4]);
 
 /* ---------------- test helpers ---------------- */

@@ -10,6 +10,8 @@
  *                                 fold_batch core.cu:25-56, fold_small core.cu:58-82)
  * plus the verifier helpers of src/ulvt/sumcheck/test/verifier.cu.
  */
+#define _POSIX_C_SOURCE 200809L
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -127,5 +129,104 @@ void orc_multilinear_composition(const uint32_t* evals_compact, int n, int d, co
 		}
 		prod = fmul(prod, acc);
 	}
+	memcpy(out, prod.w, 16);
+}
+
+/*
+ * Large-size checker for the final claim (evaluate_multilinear_composition, verifier.cu:88-107):
+ * prod_j f_j(r) with f_j(r) computed by folding the column with r[0], r[1], ..., r[n-1]
+ * (highest variable first: f(x) <- f(x) + r (f(x) + f(x + h)), which is the Lagrange-basis sum
+ * sum_x f(x) prod_v (bit v of x ? r[n-1-v] : 1 + r[n-1-v]) evaluated one variable at a time).
+ * Columns are compact, or bitsliced 128-word batches when `bitsliced`; the folds are split over
+ * `nthreads` pthreads. O(d 2^n) products instead of orc_multilinear_composition's O(d n 2^n).
+ */
+typedef struct {
+	f128* col;
+	const uint32_t* src;
+	int bitsliced;
+	size_t lo, hi, h;
+	const f128* tab; /* x -> r x as 16 byte tables: tab[256 k + b] = r (b << 8k) (linearity) */
+	int phase;       /* 0: load (untranspose), 1: fold */
+} ml_arg;
+
+static void mul_tables(f128 r, f128* tab) {
+	for (int k = 0; k < 16; k++) {
+		f128 basis[8];
+		for (int i = 0; i < 8; i++) {
+			f128 e = fconst(0);
+			e.w[(8 * k + i) / 32] = 1u << ((8 * k + i) % 32);
+			basis[i] = fmul(r, e);
+		}
+		tab[256 * k] = fconst(0);
+		for (int b = 1; b < 256; b++) {
+			const int low = __builtin_ctz((unsigned)b);
+			tab[256 * k + b] = fadd(tab[256 * k + (b & (b - 1))], basis[low]);
+		}
+	}
+}
+
+static inline f128 tab_mul(const f128* tab, f128 x) {
+	f128 acc = fconst(0);
+	for (int k = 0; k < 16; k++) acc = fadd(acc, tab[256 * k + ((x.w[k / 4] >> (8 * (k % 4))) & 0xFF)]);
+	return acc;
+}
+
+static void* ml_worker(void* p) {
+	ml_arg* a = (ml_arg*)p;
+	if (a->phase == 0) {
+		for (size_t b = a->lo; b < a->hi; b++) {
+			uint32_t blk[128];
+			memcpy(blk, a->src + 128 * b, sizeof(blk));
+			if (a->bitsliced) orc_bitslice_untranspose128(blk);
+			memcpy(a->col + 32 * b, blk, sizeof(blk));
+		}
+	} else {
+		for (size_t x = a->lo; x < a->hi; x++) a->col[x] = fadd(a->col[x], tab_mul(a->tab, fadd(a->col[x], a->col[x + a->h])));
+	}
+	return NULL;
+}
+
+static void ml_parallel(ml_arg* proto, size_t total, int nthreads) {
+	pthread_t th[256];
+	ml_arg args[256];
+	if (nthreads > 256) nthreads = 256;
+	if ((size_t)nthreads > total) nthreads = total ? (int)total : 1;
+	for (int i = 0; i < nthreads; i++) {
+		args[i] = *proto;
+		args[i].lo = total * (size_t)i / (size_t)nthreads;
+		args[i].hi = total * (size_t)(i + 1) / (size_t)nthreads;
+		pthread_create(&th[i], NULL, ml_worker, &args[i]);
+	}
+	for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+}
+
+void orc_multilinear_composition_fold_mt(const uint32_t* evals, int n, int d, int bitsliced, const uint32_t* challenges,
+                                         uint32_t out[4], int nthreads) {
+	orc_init();
+	const size_t N = (size_t)1 << n;
+	f128* col = (f128*)malloc(sizeof(f128) * (N < 32 ? 32 : N));
+	f128* tab = (f128*)malloc(sizeof(f128) * 16 * 256);
+	f128 prod = fconst(1);
+	for (int j = 0; j < d; j++) {
+		const uint32_t* src = evals + (size_t)j * 4 * N;
+		if (N < 32 || !bitsliced) {
+			memcpy(col, src, sizeof(f128) * N);
+		} else {
+			ml_arg a = {col, src, bitsliced, 0, 0, 0, NULL, 0};
+			ml_parallel(&a, N / 32, nthreads);
+		}
+		size_t cur = N;
+		for (int v = 0; v < n; v++) {
+			f128 r;
+			memcpy(r.w, challenges + 4 * (size_t)v, 16);
+			mul_tables(r, tab);
+			ml_arg a = {col, NULL, 0, 0, 0, cur / 2, tab, 1};
+			ml_parallel(&a, cur / 2, cur >= (1u << 16) ? nthreads : 1);
+			cur /= 2;
+		}
+		prod = fmul(prod, col[0]);
+	}
+	free(tab);
+	free(col);
 	memcpy(out, prod.w, 16);
 }

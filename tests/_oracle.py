@@ -44,6 +44,8 @@ def lib():
         for fn in ("orc_antt32", "orc_antt128", "orc_antt128_limbwise"):
             getattr(L, fn).restype = None
             getattr(L, fn).argtypes = [_u32p, _u32p, ctypes.c_int, ctypes.c_int]
+        L.orc_antt128_limbwise_mt.restype = None
+        L.orc_antt128_limbwise_mt.argtypes = [_u32p, _u32p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.orc_antt128_limbwise_batch.argtypes = [_u32p, _u32p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         for fn in ("orc_bitslice_transpose128", "orc_bitslice_untranspose128",
                    "orc_bitslice_transpose32", "orc_bitslice_untranspose32"):
@@ -52,6 +54,11 @@ def lib():
         L.orc_sumcheck_run.argtypes = [_u32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u32p, _u32p, _u32p]
         L.orc_sumcheck_interpolate.argtypes = [_u32p, ctypes.c_int, _u32p, _u32p]
         L.orc_multilinear_composition.argtypes = [_u32p, ctypes.c_int, ctypes.c_int, _u32p, _u32p]
+        L.orc_multilinear_composition_fold_mt.restype = None
+        L.orc_multilinear_composition_fold_mt.argtypes = [_u32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u32p, _u32p,
+                                                          ctypes.c_int]
+        L.orc_bitslice_many128.restype = None
+        L.orc_bitslice_many128.argtypes = [_u32p, ctypes.c_size_t, ctypes.c_int]
         L.orc_mt_fill.argtypes = [ctypes.c_uint32, _u32p, ctypes.c_size_t]
         L.orc_fill128.argtypes = [ctypes.c_uint32, ctypes.c_uint64, _u32p, ctypes.c_size_t]
         L.orc_md5.argtypes = [ctypes.c_void_p, ctypes.c_size_t, _u8p]
@@ -175,21 +182,15 @@ def md5_limb(v, limb):
 
 # ---------------- bitslicing ----------------
 def bitslice128(blocks):
-    b = np.array(blocks, dtype=np.uint32).reshape(-1, 128).copy()
-    for i in range(b.shape[0]):
-        row = np.ascontiguousarray(b[i])
-        lib().orc_bitslice_transpose128(row)
-        b[i] = row
-    return b.reshape(-1)
+    b = np.array(blocks, dtype=np.uint32).reshape(-1).copy()
+    lib().orc_bitslice_many128(b, b.size // 128, 0)
+    return b
 
 
 def unbitslice128(blocks):
-    b = np.array(blocks, dtype=np.uint32).reshape(-1, 128).copy()
-    for i in range(b.shape[0]):
-        row = np.ascontiguousarray(b[i])
-        lib().orc_bitslice_untranspose128(row)
-        b[i] = row
-    return b.reshape(-1)
+    b = np.array(blocks, dtype=np.uint32).reshape(-1).copy()
+    lib().orc_bitslice_many128(b, b.size // 128, 1)
+    return b
 
 
 # ---------------- sumcheck ----------------
@@ -206,6 +207,26 @@ def interpolate(points, challenge):
     p = np.ascontiguousarray(points, dtype=np.uint32).reshape(-1)
     out = np.zeros(4, np.uint32)
     lib().orc_sumcheck_interpolate(p, p.size // 4, np.ascontiguousarray(challenge, dtype=np.uint32), out)
+    return out
+
+
+def threads():
+    """Host threads for the large-size checkers (the GPU box's CPU share is 16)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    cap = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(cap) if cap.isdigit() and int(cap) > 0 else 16))
+
+
+def multilinear_composition_fold(evals, n, d, bitsliced, challenges):
+    """prod_j f_j(r) by folding (O(d 2^n) products, multithreaded); evals compact or bitsliced."""
+    out = np.zeros(4, np.uint32)
+    lib().orc_multilinear_composition_fold_mt(np.ascontiguousarray(evals, dtype=np.uint32).reshape(-1), n, d,
+                                              1 if bitsliced else 0,
+                                              np.ascontiguousarray(challenges, dtype=np.uint32).reshape(-1), out,
+                                              threads())
     return out
 
 

@@ -8,8 +8,9 @@ parsed out of the reference test sources as text (no reference code is run or ke
   bb31_ntt_md5.json      <- src/ulvt/ntt/tests/test_ntt.cu:21-50    (bb31_ntt_hashes[log_len])
   field_kats.json        <- src/ulvt/finite_fields/tests/test_fanpaartower.cu:9-273
                             src/ulvt/finite_fields/tests/tests.cu:17-201
-  sumcheck_transcripts.json / ntt128_fixtures.npz <- generated by gen_oracle_fixtures.py from
-                            the CPU oracle (self-consistency fixtures, not reference pins)
+The reference holds no GF(2^128) NTT or sumcheck vectors; those paths are pinned by the
+MD5 tables above (every limb plane of a GF(2^128) transform) and by the reference test's
+protocol invariants (tests/test_gpu_sumcheck*.py), checked against the CPU oracle.
 
 Usage: python tests/golden/make_golden.py [/root/reference]
 """

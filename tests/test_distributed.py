@@ -78,3 +78,73 @@ def _xor_worker(rank, world, port):
 def test_xor_allreduce_gloo():
     import torch.multiprocessing as mp
     mp.spawn(_xor_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def _gpu_worker(rank, world, port, n, d, seed, out_q):
+    """One rank of the world-2 GPU rehearsal: the HIP shard prover (built from this rank's share
+    only) driven by ShardedSumcheck over gloo, and this rank's slice of a batched GF(2^128) NTT.
+    Both ranks use cuda:0 (the box has one GPU)."""
+    import torch
+    import torch.distributed as dist
+
+    import binius_ntt_amd as B
+    from binius_ntt_amd.distributed import ShardedSumcheck, batch_slice
+
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda:0")
+        rng = np.random.default_rng(seed)
+        ev = rng.integers(0, 2**32, size=d * (4 << n), dtype=np.uint32)  # bitsliced columns
+        ch = rng.integers(0, 2**32, size=(n, 4), dtype=np.uint32)
+        # this rank's batches b with b mod world == rank, column by column
+        share = ev.reshape(d, (1 << n) // 32, 128)[:, rank::world, :]
+        t = torch.from_numpy(np.ascontiguousarray(share).reshape(-1).view(np.int32)).to(dev)
+        sc = ShardedSumcheck(B.Sumcheck.from_shard(n, d, t, rank, world))
+        sums, pts = [], []
+        for r in range(n + 1):
+            s, p = sc.this_round_messages()
+            sums.append(s)
+            pts.append(p)
+            if r < n:
+                sc.move_to_next_round(ch[r])
+        assert sc.replicated
+        # batched NTT: rank-contiguous slice of 6 transforms of 2^12 (no collective)
+        total, log_h = 6, 12
+        xs = np.stack([O.fill128(300 + b, 400 + b, 1 << log_h) for b in range(total)])
+        lo, hi = batch_slice(total, rank, world)
+        ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(7)))
+        xin = torch.from_numpy(xs[lo:hi].reshape(-1).view(np.int32)).to(dev)
+        yout = torch.empty_like(xin)
+        ntt.forward_device(xin, yout, batch=hi - lo)
+        torch.cuda.synchronize()
+        y = yout.cpu().numpy().view(np.uint32).reshape(hi - lo, -1, 4)
+        ntt_ok = bool(np.array_equal(y, O.antt128_batch(xs[lo:hi], log_h, 0)))
+        out_q.put((rank, np.stack(sums), np.stack(pts), ntt_ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,d", [(14, 3), (12, 2)])
+def test_sharded_hip_prover_world2_gloo(n, d, dev):
+    """World-2 gloo run of the HIP shard prover: the all-gathered + XOR-ed transcript equals the
+    oracle's unsharded transcript, every rank sees the same messages, and each rank's slice of the
+    batched NTT matches the oracle."""
+    import torch.multiprocessing as mp
+    seed = 700 + n + d
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.spawn(_gpu_worker, args=(2, _free_port(), n, d, seed, q), nprocs=2, join=True)
+    got = dict()
+    for _ in range(2):
+        rank, s, p, ok = q.get(timeout=60)
+        got[rank] = (s, p, ok)
+    rng = np.random.default_rng(seed)
+    ev = rng.integers(0, 2**32, size=d * (4 << n), dtype=np.uint32)
+    ch = rng.integers(0, 2**32, size=(n, 4), dtype=np.uint32)
+    want_s, want_p = O.sumcheck_run(ev, n, d, 1, ch)
+    for rank in (0, 1):
+        s, p, ok = got[rank]
+        assert ok, "rank %d: batched NTT slice differs from the oracle" % rank
+        assert np.array_equal(s, want_s), "rank %d: round sums" % rank
+        assert np.array_equal(p, want_p), "rank %d: round points" % rank

@@ -23,10 +23,10 @@ def test_capabilities():
     assert B.check_gpu_capabilities(), B.lib().bn_last_error()
 
 
-@pytest.mark.parametrize("log_h", list(range(1, 25)) + [pytest.param(h, marks=pytest.mark.slow) for h in range(25, 29)])
+@pytest.mark.parametrize("log_h", list(range(1, 25)) + [pytest.param(h, marks=pytest.mark.slow) for h in range(25, 31)])
 def test_gf32_r0_reference_md5(ntt_md5, log_h, dev):
-    # exactly the reference's run_and_check_additive_ntt(log_h, 0) (test_ntt.cu:191-217), up to
-    # the largest size the reference runs by default (28; 29-30 are its [slow] cases)
+    # exactly the reference's run_and_check_additive_ntt(log_h, 0) (test_ntt.cu:191-217): the
+    # default range 1-28 and its [slow] cases 29 and 30 (test_ntt.cu:231-234)
     x = O.mt_fill(0xDEADBEEF + log_h, 1 << log_h)
     ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(5)))
     inp = B.NTTData(1 << log_h, B.DataOrder.IN_ORDER, 32, x)
@@ -97,3 +97,17 @@ def test_gf128_linearity_at_2_20(dev):
     yb = _run_device(ntt, b.reshape(-1), dev)
     yab = _run_device(ntt, (a ^ b).reshape(-1), dev)
     assert np.array_equal(ya ^ yb, yab)
+
+
+@pytest.mark.slow
+def test_gf128_2p26_limb_md5_and_oracle(ntt_md5, dev):
+    # above the north-star size: limb 0 MD5-pinned by the reference table, all limbs vs the
+    # (multithreaded) oracle
+    log_h = 26
+    x = O.fill128(0xDEADBEEF + log_h, 0x5EED0000, 1 << log_h)
+    ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(7)))
+    y = _run_device(ntt, x.reshape(-1), dev).reshape(-1, 4)
+    assert O.md5_limb(y, 0) == ntt_md5["0"][log_h]
+    want = np.zeros_like(x)
+    O.lib().orc_antt128_limbwise_mt(x.reshape(-1), want.reshape(-1), log_h, 0, O.threads())
+    assert np.array_equal(y, want)

@@ -101,3 +101,28 @@ def test_sumcheck_oracle_invariants(n, d, bs):
             claim = O.interpolate(pts[r], ch[r])
     comp = O.unbitslice128(ev) if bs else ev
     assert np.array_equal(O.multilinear_composition(comp, n, d, ch), claim)
+
+
+@pytest.mark.parametrize("n,d", [(1, 1), (5, 2), (8, 3), (11, 4)])
+def test_fold_multilinear_matches_lagrange_sum(n, d):
+    # the large-size final-claim checker (fold form, multithreaded) vs the direct Lagrange-basis
+    # restatement of evaluate_multilinear_composition (verifier.cu:88-107), compact and bitsliced
+    rng = np.random.default_rng(40 + n + d)
+    ev = rng.integers(0, 2**32, size=d * (4 << n), dtype=np.uint32)
+    ch = rng.integers(0, 2**32, size=(n, 4), dtype=np.uint32)
+    want = O.multilinear_composition(ev, n, d, ch)
+    assert np.array_equal(O.multilinear_composition_fold(ev, n, d, False, ch), want)
+    if n >= 5:
+        bs = np.concatenate([O.bitslice128(c) for c in ev.reshape(d, -1)])
+        assert np.array_equal(O.multilinear_composition_fold(bs, n, d, True, ch), want)
+
+
+def test_multithreaded_ntt_matches_serial():
+    L = O.lib()
+    for log_h in (1, 6, 13):
+        x = O.fill128(11 + log_h, 12, 1 << log_h)
+        want = O.antt128(x, log_h, 0)
+        for nt in (1, 3, 8):
+            out = np.zeros_like(want)
+            L.orc_antt128_limbwise_mt(x.reshape(-1), out.reshape(-1), log_h, 0, nt)
+            assert np.array_equal(out, want), (log_h, nt)

@@ -11,6 +11,7 @@
 #include <cstring>
 #include <fstream>
 #include <iomanip>
+#include <sstream>
 #include <iostream>
 #include <map>
 #include <random>
@@ -27,6 +28,12 @@ static std::string md5hex(const void* p, size_t n) {
 	char s[33];
 	for (int i = 0; i < 16; i++) std::snprintf(s + 2 * i, 3, "%02x", d[i]);
 	return s;
+}
+
+static std::string speedup(double r) {
+	std::ostringstream o;
+	o << std::fixed << std::setprecision(3) << r << "x";
+	return o.str();
 }
 
 int main(int argc, char** argv) {
@@ -77,7 +84,7 @@ int main(int argc, char** argv) {
 		rows++;
 		for (int v = 0; v < 2; v++) pass[v] += ok[v], total[v] += ms[v];
 		std::cout << std::left << std::setw(8) << log_h << std::fixed << std::setprecision(2) << std::setw(15) << ms[0]
-				  << std::setw(15) << ms[1] << std::setprecision(3) << std::setw(12) << ms[0] / ms[1] << "x"
+				  << std::setw(15) << ms[1] << std::setw(12) << speedup(ms[0] / ms[1])
 				  << std::setw(12) << (ok[0] ? "PASS" : "FAIL") << std::setw(12) << (ok[1] ? "PASS" : "FAIL") << std::endl;
 	}
 	std::cout << "====================================================================================\n"
