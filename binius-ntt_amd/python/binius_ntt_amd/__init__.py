@@ -72,6 +72,12 @@ def lib():
         "bn_gf32_mul_device": (i32, [vp, vp, vp, sz, vp]),
         "bn_gf128_mul_repeat_device": (i32, [i32, vp, vp, sz, i32, vp]),
         "bn_bitslice_device": (i32, [vp, sz, i32, vp]),
+        "bn_multiply_unrolled": (i32, [i32, u32p, u32p, u32p]),
+        "bn_multiply_unrolled_device": (i32, [i32, vp, vp, vp, sz, vp]),
+        "bn_mul_binary_tower_32b_simd": (i32, [i32, ctypes.c_uint32, ctypes.c_uint32, u32p]),
+        "bn_interleave_32b": (i32, [i32, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p]),
+        "bn_xor_adjacent_32b": (i32, [i32, ctypes.c_uint32, u32p]),
+        "bn_packed32_device": (i32, [i32, i32, vp, vp, vp, vp, sz, vp]),
         "bn_sumcheck_create": (i32, [i32, i32, i32, i32, u32p, ctypes.POINTER(vp)]),
         "bn_sumcheck_create_device": (i32, [i32, i32, i32, i32, vp, i32, ctypes.POINTER(vp)]),
         "bn_sumcheck_round_messages": (i32, [vp, u32p, u32p]),
@@ -423,6 +429,61 @@ def bitslice(buf, untranspose=False, stream=None):
     _check_device_tensor(buf, buf.numel(), "buf")
     _check(lib().bn_bitslice_device(_ptr(buf), buf.numel() // 128, 1 if untranspose else 0,
                                     _stream(stream, _dev_index(buf))))
+
+
+def multiply_unrolled(height, a, b, dst=None):
+    """multiply_unrolled<HEIGHT> (binary_tower_unrolled.cuh:4-5) on host arrays of 2^height
+    words (32 bitsliced products); dst may be a (alias-safe). Returns dst."""
+    w = 1 << height
+    a = np.ascontiguousarray(a, dtype=np.uint32)
+    b = np.ascontiguousarray(b, dtype=np.uint32)
+    if a.size != w or b.size != w:
+        raise ValueError("operands must hold 2^height = %d words" % w)
+    if dst is None:
+        dst = np.zeros(w, np.uint32)
+    _check(lib().bn_multiply_unrolled(height, _u32p(a), _u32p(b), _u32p(dst)))
+    return dst
+
+
+def multiply_unrolled_device(height, a, b, out, stream=None):
+    """Device batch of multiply_unrolled<height> over consecutive 2^height-word blocks."""
+    _same_size("multiply_unrolled_device", a, b, out)
+    w = 1 << height
+    for t, nm in ((a, "a"), (b, "b"), (out, "out")):
+        _check_device_tensor(t, a.numel(), nm)
+    _check(lib().bn_multiply_unrolled_device(height, _ptr(a), _ptr(b), _ptr(out), a.numel() // w,
+                                             _stream(stream, _dev_index(a))))
+
+
+def mul_binary_tower_32b_simd(height, a, b):
+    """mul_binary_tower_32b_simd<HEIGHT>(a, b) (binary_tower_simd.cuh:77-127)."""
+    out = ctypes.c_uint32()
+    _check(lib().bn_mul_binary_tower_32b_simd(height, a, b, ctypes.byref(out)))
+    return out.value
+
+
+def interleave_32b(height, a, b):
+    """interleave_32b<HEIGHT>(a, b) -> (c, d) (binary_tower_simd.cuh:129-139)."""
+    c, d = ctypes.c_uint32(), ctypes.c_uint32()
+    _check(lib().bn_interleave_32b(height, a, b, ctypes.byref(c), ctypes.byref(d)))
+    return c.value, d.value
+
+
+def xor_adjacent_32b(height, a):
+    """xor_adjacent_32b<HEIGHT>(a) (binary_tower_simd.cuh:141-150)."""
+    out = ctypes.c_uint32()
+    _check(lib().bn_xor_adjacent_32b(height, a, ctypes.byref(out)))
+    return out.value
+
+
+def packed32_device(op, height, a, b=None, c=None, d=None, stream=None):
+    """Device batch of the packed-word primitives: op 0 multiply, 1 interleave, 2 xor_adjacent."""
+    n = a.numel()
+    for t, nm in ((a, "a"), (b, "b"), (c, "c"), (d, "d")):
+        if t is not None:
+            _check_device_tensor(t, n, nm)
+    _check(lib().bn_packed32_device(op, height, _ptr(a), _ptr(b) if b is not None else None,
+                                    _ptr(c), _ptr(d) if d is not None else None, n, _stream(stream, _dev_index(a))))
 
 
 # ------------------------------------------------------------------ sumcheck

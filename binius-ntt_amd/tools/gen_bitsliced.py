@@ -191,6 +191,204 @@ class Emitter:
         return lines
 
 
+class LutEmitter:
+    """Technology mapping of the AND/XOR DAG onto gfx950's v_bitop3_b32, which evaluates ANY
+    3-input boolean function in one VALU instruction: enumerate the 3-feasible cuts of every node,
+    pick a cover by area flow (a node whose value several cuts would recompute is kept when that
+    is cheaper, re-derived inside each consumer's 3-input function when it is not), refine with
+    the mapping's real reference counts, and emit one instruction per chosen cut with its truth
+    table as the bitop3 immediate (imm bit (a<<2 | b<<1 | c) = f(a, b, c)). The result is
+    checked against the DAG by random simulation before it is written."""
+
+    K = 3
+    CUTS_PER_NODE = 16
+
+    def __init__(self, dag, roots):
+        self.d = dag
+        self.roots = [r for r in roots if r is not None]
+
+    def _live(self):
+        d = self.d
+        live = set()
+        stack = list(self.roots)
+        while stack:
+            n = stack.pop()
+            if n in live:
+                continue
+            live.add(n)
+            op, args = d.nodes[n]
+            if op != "in":
+                stack.extend(args)
+        return sorted(live)
+
+    def _cuts(self, order):
+        d = self.d
+        cuts = {}
+        for n in order:
+            op, args = d.nodes[n]
+            if op == "in":
+                cuts[n] = [frozenset([n])]
+                continue
+            a, b = args
+            cs = set()
+            for ca in cuts[a]:
+                for cb in cuts[b]:
+                    u = ca | cb
+                    if len(u) <= self.K:
+                        cs.add(u)
+            cs = sorted(cs, key=lambda c: (len(c), sorted(c)))[: self.CUTS_PER_NODE]
+            cuts[n] = cs + [frozenset([n])]
+        return cuts
+
+    def _map(self, order, cuts, refs):
+        d = self.d
+        af = {}
+        best = {}
+        for n in order:
+            if d.nodes[n][0] == "in":
+                af[n] = 0.0
+                continue
+            bc, bv = None, None
+            for c in cuts[n]:
+                if n in c:
+                    continue
+                v = 1.0 + sum(af[l] / max(1, refs.get(l, 1)) for l in c)
+                if bv is None or v < bv - 1e-9 or (abs(v - bv) <= 1e-9 and len(c) < len(bc)):
+                    bc, bv = c, v
+            best[n] = bc
+            af[n] = bv
+        mapped = {}
+        need = list(self.roots)
+        while need:
+            n = need.pop()
+            if n in mapped or d.nodes[n][0] == "in":
+                continue
+            mapped[n] = best[n]
+            need.extend(best[n])
+        return mapped
+
+    def _truth(self, n, leaves):
+        d = self.d
+        pats = (0xF0, 0xCC, 0xAA)
+        val = {l: pats[i] for i, l in enumerate(leaves)}
+
+        def ev(x):
+            if x in val:
+                return val[x]
+            op, args = d.nodes[x]
+            va, vb = ev(args[0]), ev(args[1])
+            r = (va & vb) if op == "and" else (va ^ vb)
+            val[x] = r
+            return r
+        return ev(n) & 0xFF
+
+    def build(self):
+        order = self._live()
+        cuts = self._cuts(order)
+        refs = {}
+        for n in order:
+            op, args = self.d.nodes[n]
+            if op != "in":
+                for a in args:
+                    refs[a] = refs.get(a, 0) + 1
+        mapped = self._map(order, cuts, refs)
+        for _ in range(3):  # re-estimate fanouts from the current cover
+            refs = {}
+            for n, c in mapped.items():
+                for l in c:
+                    refs[l] = refs.get(l, 0) + 1
+            for r in self.roots:
+                refs[r] = refs.get(r, 0) + 1
+            m2 = self._map(order, cuts, refs)
+            if len(m2) >= len(mapped):
+                break
+            mapped = m2
+        self.mapped = mapped
+        return mapped
+
+    def emit(self, input_map, outputs, barrier_every=0):
+        mapped = self.build()
+        d = self.d
+        name = {}
+        lines = []
+        cnt = 0
+        for n in sorted(mapped):
+            leaves = sorted(mapped[n])
+            tt = self._truth(n, leaves)
+            args = []
+            for l in leaves:
+                args.append(input_map[d.nodes[l][1][0]] if d.nodes[l][0] == "in" else name[l])
+            v = "t%d" % cnt
+            cnt += 1
+            if len(leaves) == 2 and tt == 0xF0 ^ 0xCC:
+                expr = "%s ^ %s" % tuple(args)
+            elif len(leaves) == 2 and tt == 0xF0 & 0xCC:
+                expr = "%s & %s" % tuple(args)
+            else:
+                while len(args) < 3:
+                    args.append(args[0])  # the truth table ignores the padding operand
+                expr = "BN_BITOP3(%s, %s, %s, 0x%02x)" % (args[0], args[1], args[2], tt)
+            lines.append("const uint32_t %s = %s;" % (v, expr))
+            name[n] = v
+            if barrier_every and cnt % barrier_every == 0:
+                lines.append("BN_SCHED_BARRIER();")
+        for lv, r in outputs:
+            if r is None:
+                lines.append("%s = 0u;" % lv)
+            elif d.nodes[r][0] == "in":
+                lines.append("%s = %s;" % (lv, input_map[d.nodes[r][1][0]]))
+            else:
+                lines.append("%s = %s;" % (lv, name[r]))
+        self._selfcheck(outputs)
+        return lines
+
+    def _selfcheck(self, outputs, trials=4):
+        """Random 64-bit simulation: the mapped network equals the DAG on every output."""
+        import random
+        d = self.d
+        rnd = random.Random(1234)
+        for _ in range(trials):
+            ref = {}
+            for i, (op, args) in enumerate(d.nodes):
+                if op == "in":
+                    ref[i] = rnd.getrandbits(64)
+            inputs = dict(ref)
+
+            def ev_ref(x):
+                if x in ref:
+                    return ref[x]
+                op, args = d.nodes[x]
+                a, b = ev_ref(args[0]), ev_ref(args[1])
+                ref[x] = (a & b) if op == "and" else (a ^ b)
+                return ref[x]
+            got = dict(inputs)
+            for n in sorted(self.mapped):
+                leaves = sorted(self.mapped[n])
+                tt = self._truth(n, leaves)
+                vals = [got[l] for l in leaves]
+                while len(vals) < 3:
+                    vals.append(vals[0])
+                a, b, c = vals
+                r = 0
+                for i in range(8):
+                    if (tt >> i) & 1:
+                        ma = a if (i >> 2) & 1 else ~a
+                        mb = b if (i >> 1) & 1 else ~b
+                        mc = c if i & 1 else ~c
+                        r |= ma & mb & mc
+                got[n] = r & ((1 << 64) - 1)
+            for _, r in outputs:
+                if r is not None and got[r] != ev_ref(r):
+                    raise AssertionError("LUT mapping differs from the DAG")
+
+
+EMITTER = os.environ.get("BN_GEN_EMITTER", "lut")
+
+
+def make_emitter(dag, roots):
+    return LutEmitter(dag, roots) if EMITTER == "lut" else Emitter(dag, roots)
+
+
 def count_ops(lines):
     return sum(1 for l in lines if l.startswith("const uint32_t t"))
 
@@ -199,7 +397,7 @@ def gen_prep(h):
     d = DAG()
     w = [d.inp("w%d" % i) for i in range(1 << h)]
     leaves = presums(d, w, h)
-    e = Emitter(d, leaves)
+    e = make_emitter(d, leaves)
     body = e.emit({"w%d" % i: "w[%d]" % i for i in range(1 << h)},
                   [("wl[%d]" % i, leaves[i]) for i in range(len(leaves))])
     return body
@@ -218,7 +416,7 @@ def gen_mulp(h, accumulate=False):
         acc = [d.inp("o%d" % i) for i in range(n)]
         imap.update({"o%d" % i: "o%d_" % i for i in range(n)})
         res = [d.xor(r, a) for r, a in zip(res, acc)]
-    e = Emitter(d, res)
+    e = make_emitter(d, res)
     body = e.emit(imap, [("out[%d]" % i, res[i]) for i in range(n)])
     pre = ["const uint32_t x%d_ = x[%d];" % (i, i) for i in range(n)]
     if accumulate:
@@ -242,7 +440,7 @@ def gen_full(h, accumulate=False):
         acc = [d.inp("o%d" % i) for i in range(n)]
         imap.update({"o%d" % i: "o%d_" % i for i in range(n)})
         res = [d.xor(r, q) for r, q in zip(res, acc)]
-    e = Emitter(d, res)
+    e = make_emitter(d, res)
     body = e.emit(imap, [("out[%d]" % i, res[i]) for i in range(n)], BARRIER_EVERY if h <= 5 else 0)
     pre = ["const uint32_t a%d_ = a[%d];" % (i, i) for i in range(n)]
     pre += ["const uint32_t b%d_ = b[%d];" % (i, i) for i in range(n)]
@@ -252,16 +450,32 @@ def gen_full(h, accumulate=False):
 
 
 def fn(sig, lines):
-    return "__device__ __forceinline__ " + sig + " {\n\t" + "\n\t".join(lines) + "\n}\n"
+    # host + device: the device build maps BN_BITOP3 onto v_bitop3_b32, the host build (the
+    # reference's __host__ multiply_unrolled<H>, binary_tower_unrolled.cuh:4-5) onto plain logic
+    return "__host__ __device__ __forceinline__ " + sig + " {\n\t" + "\n\t".join(lines) + "\n}\n"
 
 
 def main():
     parts = ["// GENERATED by binius-ntt_amd/tools/gen_bitsliced.py -- do not edit.",
              "// Bitsliced binary-tower multipliers (Karatsuba tower, gfx950 v_bitop3 fusion).",
              "#pragma once", "#include <hip/hip_runtime.h>", "#include <stdint.h>", "",
-             "#define BN_XOR3(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x96)",
-             "#define BN_ANDXOR(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x6a)",
-             "#define BN_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)", "",
+             "// BN_BITOP3(a, b, c, imm): any 3-input boolean function, imm bit (a<<2 | b<<1 | c) = f(a, b, c)",
+             "#if defined(__HIP_DEVICE_COMPILE__)",
+             "#define BN_BITOP3(a, b, c, imm) __builtin_amdgcn_bitop3_b32((a), (b), (c), (imm))",
+             "#define BN_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)",
+             "#else",
+             "__host__ __device__ constexpr uint32_t bn_bitop3_host(uint32_t a, uint32_t b, uint32_t c, unsigned imm) {",
+             "\tuint32_t r = 0;",
+             "\tfor (unsigned i = 0; i < 8; i++)",
+             "\t\tif ((imm >> i) & 1u) r |= ((i & 4u) ? a : ~a) & ((i & 2u) ? b : ~b) & ((i & 1u) ? c : ~c);",
+             "\treturn r;",
+             "}",
+             "#define BN_BITOP3(a, b, c, imm) bn_bitop3_host((a), (b), (c), (imm))",
+             "#define BN_SCHED_BARRIER()",
+             "#endif",
+             "#define BN_XOR3(a, b, c) BN_BITOP3((a), (b), (c), 0x96)",
+             "#define BN_ANDXOR(a, b, c) BN_BITOP3((a), (b), (c), 0x6a)",
+             "",
              "namespace bn {", ""]
     stats = []
     for h in (2, 3, 4, 5):
@@ -275,12 +489,12 @@ def main():
         parts.append("// mulp_acc (out ^= x*w): %d gates" % count_ops(al))
         parts.append(fn("void bsm%d_mulp_acc(const uint32_t* x, const uint32_t* __restrict__ wl, uint32_t* out)" % h, al))
         stats.append((h, count_ops(pl), count_ops(ml), count_ops(al)))
-    for h in (3, 4, 5, 7):
+    for h in (2, 3, 4, 5, 6, 7):
         fl = gen_full(h)
         parts.append("// full multiply: %d gates for 32 products" % count_ops(fl))
         parts.append(fn("void bsm%d_mul(const uint32_t* a, const uint32_t* b, uint32_t* out)" % h, fl))
         stats.append((h, "full", count_ops(fl)))
-        if h < 7:
+        if 3 <= h < 6:
             fa = gen_full(h, accumulate=True)
             parts.append("// full multiply-accumulate (out ^= a*b): %d gates" % count_ops(fa))
             parts.append(fn("void bsm%d_mul_acc(const uint32_t* a, const uint32_t* b, uint32_t* out)" % h, fa))

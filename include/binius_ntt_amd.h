@@ -120,6 +120,27 @@ int bn_gf128_mul_repeat_device(int kind, void* d_state, const void* d_operand, s
 int bn_bitslice_device(void* d_buf, size_t n_blocks, int untranspose, void* stream);
 
 /* ------------------------------------------------------------------------------------
+ * Field primitives beside the hot path (src/ulvt/finite_fields)
+ * ------------------------------------------------------------------------------------ */
+/* Replaces multiply_unrolled<HEIGHT>(a, b, dst) (circuit_generator/unrolled/
+ * binary_tower_unrolled.cuh:4-5): 32 bitsliced GF(2^(2^height)) products, 2^height words per
+ * operand (word i = bit i of the 32 elements). Host computation; alias-safe (dst may be a or b,
+ * as core.cu:21 uses it). 2 <= height <= 7. */
+int bn_multiply_unrolled(int height, const uint32_t* a, const uint32_t* b, uint32_t* dst);
+/* Device batch of the same: nblocks blocks of 2^height words per operand. Async on `stream`. */
+int bn_multiply_unrolled_device(int height, const void* a, const void* b, void* dst, size_t nblocks, void* stream);
+/* Replaces mul_binary_tower_32b_simd<HEIGHT>(a, b) (binary_tower_simd.cuh:77-127): the words as
+ * 32/2^height packed GF(2^(2^height)) elements, multiplied lane by lane. 0 <= height <= 5. */
+int bn_mul_binary_tower_32b_simd(int height, uint32_t a, uint32_t b, uint32_t* out);
+/* Replaces interleave_32b<HEIGHT>(a, b) -> (c, d) and xor_adjacent_32b<HEIGHT>(a)
+ * (binary_tower_simd.cuh:129-150); 0 <= height <= 4. */
+int bn_interleave_32b(int height, uint32_t a, uint32_t b, uint32_t* c, uint32_t* d);
+int bn_xor_adjacent_32b(int height, uint32_t a, uint32_t* out);
+/* Device batch over n words: op 0 = mul_binary_tower_32b_simd (c = a*b), 1 = interleave_32b
+ * ((c, d) from (a, b)), 2 = xor_adjacent_32b (c from a; b, d unused). Async on `stream`. */
+int bn_packed32_device(int op, int height, const void* a, const void* b, void* c, void* d, size_t n, void* stream);
+
+/* ------------------------------------------------------------------------------------
  * Sumcheck over GF(2^128) (src/ulvt/sumcheck/sumcheck.cuh:10-301)
  * ------------------------------------------------------------------------------------ */
 typedef struct bn_sumcheck bn_sumcheck;

@@ -12,6 +12,8 @@
 #include <vector>
 
 #include "finite_fields/binary_tower.hpp"
+#include "finite_fields/binary_tower_simd.hpp"
+#include "finite_fields/circuit_generator/unrolled/binary_tower_unrolled.hpp"
 #include "ntt/additive_ntt.hpp"
 #include "sumcheck/sumcheck.hpp"
 #include "sumcheck/verifier.hpp"
@@ -107,6 +109,64 @@ static void bitslicing() {
 	check(ok, "BitsliceUtils<128> transpose / untranspose vs oracle");
 }
 
+// multiply_unrolled<H> (binary_tower_unrolled.cuh:4-5, in place as core.cu:21 calls it) and the
+// packed-subfield operations (binary_tower_simd.cuh:77-150, KATs of tests.cu:17-95) vs the oracle
+template <int H>
+static bool unrolled_vs_oracle(std::mt19937& g) {
+	constexpr int W = 1 << H;
+	uint32_t a[W], b[W];
+	for (auto& w : a) w = g();
+	for (auto& w : b) w = g();
+	uint32_t dst[W];
+	std::memcpy(dst, a, sizeof(a));
+	multiply_unrolled<H>(dst, b, dst);
+	bool ok = true;
+	for (int e = 0; e < 32; e++) {
+		uint64_t x = 0, y = 0, z = 0;
+		for (int i = 0; i < W && i < 64; i++) {
+			x |= (uint64_t)((a[i] >> e) & 1) << i;
+			y |= (uint64_t)((b[i] >> e) & 1) << i;
+			z |= (uint64_t)((dst[i] >> e) & 1) << i;
+		}
+		if (H <= 6) ok = ok && orc_mul(x, y, H) == z;
+	}
+	return ok;
+}
+
+static void field_simd() {
+	std::mt19937 g(77);
+	bool ok = unrolled_vs_oracle<2>(g) && unrolled_vs_oracle<5>(g) && unrolled_vs_oracle<6>(g);
+	// H = 7: 32 GF(2^128) products through BitsliceUtils<128> vs orc_mul128
+	uint32_t a[128], b[128], c[128];
+	for (auto& w : a) w = g();
+	for (auto& w : b) w = g();
+	uint32_t as[128], bs[128];
+	std::memcpy(as, a, sizeof(a));
+	std::memcpy(bs, b, sizeof(b));
+	BitsliceUtils<128>::bitslice_transpose(as);
+	BitsliceUtils<128>::bitslice_transpose(bs);
+	multiply_unrolled<7>(as, bs, c);
+	BitsliceUtils<128>::bitslice_untranspose(c);
+	for (int e = 0; e < 32; e++) {
+		uint32_t r[4];
+		orc_mul128(a + 4 * e, b + 4 * e, r);
+		ok = ok && std::memcmp(r, c + 4 * e, 16) == 0;
+	}
+	check(ok, "multiply_unrolled<2,5,6,7> (in place) vs oracle");
+	ok = mul_binary_tower_32b_simd<5>(0xd82c07cdu, 0xd82c07cdu) == 0xafab1b8fu &&
+	     mul_binary_tower_32b_simd<3>(0xe0u, 0x76u) == 0x96u && mul_binary_tower_32b_simd<4>(0x4f4bu, 0x4386u) == 0x7202u;
+	for (int i = 0; i < 64; i++) {
+		const uint32_t x = g(), y = g();
+		ok = ok && mul_binary_tower_32b_simd<5>(x, y) == orc_mul32(x, y);
+	}
+	const auto cd = interleave_32b<0>(0x0000ffffu, 0xffff0000u);
+	ok = ok && cd.first == 0xaaaa5555u && cd.second == 0xaaaa5555u;
+	const auto ab = interleave_32b<4>(0x11100100u, 0x13120302u);
+	ok = ok && ab.first == 0x03020100u && ab.second == 0x13121110u;
+	ok = ok && xor_adjacent_32b<3>(0x0000ff0fu) == 0x0000f0f0u;
+	check(ok, "mul_binary_tower_32b_simd / interleave_32b / xor_adjacent_32b");
+}
+
 // test.cu:13-101 with fixed seeds: per-round verifier checks and the final brute-force claim
 template <uint32_t N, uint32_t D, bool T>
 static void sumcheck_protocol() {
@@ -180,6 +240,7 @@ int main() {
 	apply_rejects();
 	field_policies();
 	bitslicing();
+	field_simd();
 	sumcheck_protocol<12, 3, true>();
 	sumcheck_protocol<11, 2, false>();
 	sumcheck_protocol<10, 4, true>();

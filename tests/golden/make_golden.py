@@ -88,6 +88,19 @@ def field_kats():
     words = [int(v, 16) for _, v in sorted(res)]
     c = sum(w << (32 * i) for i, w in enumerate(words))
     kats["mul128"] = [[int(sa, 16), int(sb, 16), c]]
+    # packed-subfield products at heights 0, 2, 5 (tests.cu:68-95) and the interleave_32b KATs
+    # (tests.cu:17-53: a/b/c/d assignments followed by REQUIREs in both directions)
+    for h, a, b, c in re.findall(r"mul_binary_tower_32b_simd<(\d)>\((0x[0-9a-f]+),\s*(0x[0-9a-f]+)\)\s*==\s*(0x[0-9a-f]+)", t):
+        kats.setdefault("simd_h%s" % h, []).append([int(a, 16), int(b, 16), int(c, 16)])
+    blk = t[t.index('TEST_CASE("interleave_32b"'):t.index('TEST_CASE("interleave"')]
+    env = {}
+    kats["interleave32"] = []
+    for m in re.finditer(r"(\w) = (0x[0-9a-f]+);|REQUIRE\(interleave_32b<(\d)>\((\w), (\w)\) == make_pair\((\w), (\w)\)\)", blk):
+        if m.group(1):
+            env[m.group(1)] = int(m.group(2), 16)
+        else:
+            h, x, y, u, v = m.group(3), m.group(4), m.group(5), m.group(6), m.group(7)
+            kats["interleave32"].append([int(h), env[x], env[y], env[u], env[v]])
     return kats
 
 
@@ -102,6 +115,6 @@ if __name__ == "__main__":
                              "MD5 over output asUInt32() words (test_ntt.cu:126-152)",
                    "hashes": bb31_hashes()}, f, indent=1)
     with open(os.path.join(HERE, "field_kats.json"), "w") as f:
-        json.dump({"source": "src/ulvt/finite_fields/tests/test_fanpaartower.cu:9-273, tests.cu:172-201",
+        json.dump({"source": "src/ulvt/finite_fields/tests/test_fanpaartower.cu:9-273, tests.cu:17-95,172-201",
                    "kats": field_kats()}, f, indent=1)
     print("wrote", os.listdir(HERE))
