@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--sc-log-n", type=int, default=28)
     ap.add_argument("--sc-d", type=int, default=3)
     ap.add_argument("--sc-runs", type=int, default=2)
+    ap.add_argument("--variant", type=int, default=None, help="NTT kernel variant (default: the plan's choice)")
     return ap.parse_args()
 
 
@@ -201,16 +202,21 @@ def main():
     del x
     d_out = torch.empty_like(d_in)
     ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(7), device=local))
+    if a.variant is not None:
+        ntt.set_variant(a.variant)
     for _ in range(a.warmup):
         ntt.forward_device(d_in, d_out, stream=stream)
     torch.cuda.synchronize(dev)
 
-    # per-pass durations: each pass launched back to back on the launch stream between two
-    # hipEvents (steady-state duration per launch, as in the timed loop; bn_antt_time_passes)
-    scratch = torch.empty_like(d_out)
-    pass_ms = ntt.time_passes(d_in, scratch, reps=max(5, min(a.steps, 20)), stream=stream)
-    del scratch
+    # per-pass durations inside the back-to-back transform loop: hipEvents recorded between the
+    # pass launches of consecutive transforms (no host synchronisation between launches), averaged
+    # per pass; profiles/r02 holds the rocprofv3 kernel trace of the same loop for comparison
+    ntt.set_event_timing(True)
+    for _ in range(max(5, min(a.steps, 20))):
+        ntt.forward_device(d_in, d_out, stream=stream)
     torch.cuda.synchronize(dev)
+    pass_ms = ntt.event_timing()
+    ntt.set_event_timing(False)
 
     dt = timed(lambda: ntt.forward_device(d_in, d_out, stream=stream), a.steps)
     ms_step = dt / a.steps * 1e3
@@ -279,6 +285,8 @@ def main():
         bt_in = torch.randint(-2**31, 2**31 - 1, (max(mine, 1) * 4 * nb,), dtype=torch.int32, device=dev)
         bt_out = torch.empty_like(bt_in)
         bplan = B.AdditiveNTT(B.AdditiveNTTConf(a.c5_log_n, 0, B.FanPaarTowerField(7), device=local))
+        if a.variant is not None:
+            bplan.set_variant(a.variant)
 
         def run_batch():
             if mine:

@@ -354,9 +354,9 @@ extern "C" int bn_antt_plan_query(const bn_antt_plan* p, int what, int64_t* valu
 
 extern "C" int bn_antt_plan_set_variant(bn_antt_plan* p, int variant) {
 	BN_CHECK_ARG(p != nullptr, "plan is NULL");
-	BN_CHECK_ARG(variant == 0 || variant == 1, "variant must be 0 or 1");
-	if (variant == 1 && !bs_supports(p)) BN_FAIL(BN_ERR_UNSUPPORTED, "variant 1 needs log_h >= 12");
-	if (variant == 1 && p->variant != 1) {
+	BN_CHECK_ARG(variant >= 0 && variant <= 2, "variant must be 0, 1 or 2");
+	if (variant != 0 && !bs_supports(p)) BN_FAIL(BN_ERR_UNSUPPORTED, "variants 1 and 2 need log_h >= 12");
+	if (variant != 0 && p->variant == 0) {
 		int prev = 0;
 		hipGetDevice(&prev);
 		BN_HIP(hipSetDevice(p->device));
@@ -383,7 +383,7 @@ extern "C" int bn_antt_time_passes(bn_antt_plan* p, const void* d_in, void* d_ou
 	BN_CHECK_ARG(p != nullptr && d_in != nullptr && d_out != nullptr && ms_per_pass != nullptr && n_passes != nullptr,
 	             "NULL argument");
 	BN_CHECK_ARG(batch >= 1 && reps >= 1, "batch and reps must be >= 1");
-	if (p->variant != 1) BN_FAIL(BN_ERR_UNSUPPORTED, "pass timing is built for kernel variant 1");
+	if (p->variant == 0) BN_FAIL(BN_ERR_UNSUPPORTED, "pass timing is built for kernel variants 1 and 2");
 	int dev_prev = 0;
 	hipGetDevice(&dev_prev);
 	if (dev_prev != p->device) BN_HIP(hipSetDevice(p->device));

@@ -108,6 +108,28 @@ __device__ __forceinline__ void mul_tw(int field, const uint32_t* x, const uint3
 	}
 }
 
+// out = t*x for 32 bitsliced GF(2^32) limbs and a per-lane scalar twiddle t (same field rules as
+// mul_tw): the twiddle's Karatsuba w-side leaves are packed bits (bsmN_wpack) extracted at their
+// use, so no 32-word broadcast array is live during the circuit (~40 fewer VGPRs).
+template <int FMAX>
+__device__ __forceinline__ void mul_tw_packed(int field, const uint32_t* x, uint32_t t, uint32_t* out) {
+	if (FMAX <= 8 || field <= 8) {
+		uint32_t wp[kBsm3PackWords];
+		bsm3_wpack(t, wp);
+#pragma unroll
+		for (int g = 0; g < 4; g++) bsm3_mulpk(x + 8 * g, wp, out + 8 * g);
+	} else if (FMAX <= 16 || field <= 16) {
+		uint32_t wp[kBsm4PackWords];
+		bsm4_wpack(t, wp);
+#pragma unroll
+		for (int g = 0; g < 2; g++) bsm4_mulpk(x + 16 * g, wp, out + 16 * g);
+	} else {
+		uint32_t wp[kBsm5PackWords];
+		bsm5_wpack(t, wp);
+		bsm5_mulpk(x, wp, out);
+	}
+}
+
 // LDS image of a tile: one plane per limb, block q of limb l at l*kPlane + q*kLimbStride (stride 36
 // words: 16 consecutive blocks of one plane hit 16 distinct 4-bank groups, so a wave's
 // ds_read_b128 over consecutive blocks is conflict-free).
@@ -538,6 +560,8 @@ bool bs_supports(const bn_antt_plan* plan) {
 	return plan->log_h >= kMinLogH && plan->log_h - 5 - kBlkBits <= kMaxOuter && plan->log_rate <= kMaxRateBits;
 }
 
+static int rt_prepare();
+
 int bs_prepare(bn_antt_plan* plan) {
 	for (int L : {1, 4})
 		for (int role = 0; role < 4; role++)
@@ -545,6 +569,8 @@ int bs_prepare(bn_antt_plan* plan) {
 				for (int pf = 0; pf < 2; pf++)
 					BN_HIP(hipFuncSetAttribute(kernel_for(L, role, f, pf != 0), hipFuncAttributeMaxDynamicSharedMemorySize,
 					                           (int)lds_bytes(L)));
+	int rc = rt_prepare();
+	if (rc != BN_OK) return rc;
 	int cus = 0;
 	BN_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, plan->device));
 	plan->num_cus = std::max(cus, 1);
@@ -587,8 +613,12 @@ static BsDevKnobs dev_knobs() {
 }
 
 // one launch of pass i of the transform
+static int launch_rt(bn_antt_plan* plan, const BsPass& pass, int i, const uint32_t* d_in, uint32_t* d_out, size_t batch,
+                     hipStream_t st, const BsDevKnobs& kn);
+
 static int launch_one(bn_antt_plan* plan, const BsPass& pass, int i, const uint32_t* d_in, uint32_t* d_out,
                       size_t batch, hipStream_t st, const BsDevKnobs& kn) {
+	if (plan->variant == 2) return launch_rt(plan, pass, i, d_in, d_out, batch, st, kn);
 	const int L = plan->limbs;
 	BsParams prm;
 	prm.src = d_in;
@@ -641,6 +671,488 @@ int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t 
 	for (size_t i = 0; i < npass; i++) {
 		int rc = launch_one(plan, passes[i], (int)i, d_in, d_out, batch, st, kn);
 		if (rc != BN_OK) return rc;
+	}
+	return BN_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// Kernel variant 2: register-resident tiles
+// ------------------------------------------------------------------------------------
+//
+// Same passes, tiles and HBM layouts as variant 1, but the stages run on registers. Wave w of a
+// work-group owns limb plane w of the tile; lane L holds two bitsliced blocks R0, R1 (64 VGPRs).
+// The 7 tile bits are carried by the register index (one bit) and six lane coordinates
+//   c0 = L0^L2, c1 = L1^L2, c2 = L2, c3 = L3, c4 = L4, c5 = L5,
+// whose partner lanes (L ^ 1, 2, 7, 8, 16, 32) are one DPP quad_perm, row_half_mirror or
+// row_ror:8 read, or a gfx950 v_permlane16/32_swap. A stage always pairs R0 with R1 of the same
+// lane: before the stage on tile bit m the register bit is exchanged with lane coordinate m
+// (a transposition: lanes with c_m = 0 keep R0 and take the partner's R0 into R1, lanes with
+// c_m = 1 keep R1 and take the partner's R1 into R0), so the butterfly itself is lane-private
+// (R0 ^= t*R1, R1 ^= R0) and no stage touches LDS. LDS only stages the coalesced tile load
+// and store (and the limb interleave of compact data).
+constexpr int kRtPlane = kTileBlocks * kLimbStride + 32;  // words; the +32 staggers planes by half the banks
+constexpr int kRtOutPlane = 4096 + 256;                    // compact out: element e at e + 4*(e >> 6)
+
+struct RtPass {
+	int lo, k, role, n_outer, mlow;
+	int bb[kBlkBits];
+	int ob[kMaxOuter];
+	int jm[kBlkBits];       // stage index (s - lo) of the block stage on tile bit m, -1 if none
+	int field_m[kBlkBits];  // its twiddle sub-field
+	int field_s[5];         // in-word stages s = 0..4 (bottom pass)
+	uint32_t tau[kBlkBits][6];  // block stage on tile bit m: twiddle contribution of lane bit b
+	uint32_t tau_iw[5][6];      // in-word stage s: lane-bit contributions to block R1's twiddle
+	uint32_t cb_const[5];       // in-word stage s: R1's tile-bit-0 contribution
+	uint32_t two[kMaxStages][kMaxOuter];
+	uint32_t twc[kMaxStages][kMaxRateBits];
+	uint32_t pat[5][32];  // in-word stage s: bit-lane part of the twiddle words (R0/R1 difference folded)
+};
+
+struct RtParams {
+	const uint32_t* src;
+	uint32_t* dst;
+	int log_h, log_rate;
+	unsigned long long* trace;  // development build (BN_DEV) only: per-wave phase timestamps
+	int dbg;                    // development build only: 1 no global loads, 2 no global stores
+	RtPass p;
+};
+
+#ifdef BN_DEV
+#define RT_TS(k)                                                                 \
+	if (P.trace) {                                                               \
+		asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");              \
+		ts[k] = __builtin_amdgcn_s_memtime();                                    \
+	}
+#define RT_DBG(f) (P.dbg & (f))
+#else
+#define RT_TS(k)
+#define RT_DBG(f) false
+#endif
+
+// Lane-coordinate transposition with the register bit: lanes with c_m = 1 (mk all ones) keep R1
+// and take the partner's R1 into R0, lanes with c_m = 0 keep R0 and take the partner's R0 into R1.
+// The partner read is a ds_bpermute (LDS crossbar, no LDS memory) with a per-lane source address, so
+// one code path serves every coordinate (partner L ^ pi_m) and the identity (pi = 0, mk = 0) the
+// stage on tile bit 6 uses. Selects are v_bitop3 m ? a : b on the lane mask (a C select of two
+// array elements can become a select of their addresses, which would keep R0/R1 out of registers).
+__device__ __forceinline__ void rt_swap(uint32_t* R0, uint32_t* R1, uint32_t mk, int paddr) {
+#pragma unroll
+	for (int i = 0; i < 32; i++) {
+		const uint32_t s = __builtin_amdgcn_bitop3_b32(mk, R0[i], R1[i], 0xca);
+		const uint32_t x = (uint32_t)__builtin_amdgcn_ds_bpermute(paddr, (int)s);
+		R0[i] = __builtin_amdgcn_bitop3_b32(mk, x, R0[i], 0xca);
+		R1[i] = __builtin_amdgcn_bitop3_b32(mk, R1[i], x, 0xca);
+	}
+}
+
+// register arrays are filled and drained component-wise (no uint4 punning, which keeps them out of scratch)
+__device__ __forceinline__ void rt_unpack(uint32_t* r, uint4 v) {
+	r[0] = v.x;
+	r[1] = v.y;
+	r[2] = v.z;
+	r[3] = v.w;
+}
+__device__ __forceinline__ uint4 rt_pack(const uint32_t* r) { return make_uint4(r[0], r[1], r[2], r[3]); }
+
+// Upper passes whose twiddles all lie in GF(2^8) need far fewer registers than the GF(2^32)
+// circuit: they stage the tile through LDS in two halves (37 KB per work-group instead of 74 KB)
+// and run three work-groups per CU, so one work-group's loads and stores overlap the others' stages.
+template <int ROLE, int FMAX>
+struct RtCfg {
+	static constexpr bool LAST = ROLE == ROLE_LAST || ROLE == ROLE_SINGLE;
+	static constexpr bool HALF = !LAST && FMAX <= 8;
+	static constexpr int OCC = HALF ? 3 : 2;
+	static constexpr bool PARK = true;  // idle blocks wait in LDS during the multiplies (register pressure)
+	static constexpr int PLANE = HALF ? (kTileBlocks / 2) * kLimbStride + 32 : kRtPlane;
+};
+
+template <int L, int ROLE, int FMAX>
+__global__ __launch_bounds__(64 * L, (RtCfg<ROLE, FMAX>::OCC)) void antt_rt_pass(RtParams P) {
+	extern __shared__ uint32_t lds[];
+	using C = RtCfg<ROLE, FMAX>;
+	constexpr int NT = 64 * L;
+	constexpr bool IN_COMPACT = ROLE == ROLE_FIRST || ROLE == ROLE_SINGLE;
+	constexpr bool LAST = C::LAST;
+	constexpr bool HALF = C::HALF;
+	constexpr int PL = C::PLANE;
+	const RtPass& ps = P.p;
+	const int tid = threadIdx.x;
+	const int w = tid >> 6, lane = tid & 63;
+	const size_t n = (size_t)1 << P.log_h;
+#ifdef BN_DEV
+	unsigned long long ts[5] = {0, 0, 0, 0, 0};
+#endif
+	RT_TS(0);
+
+	// tile -> (outer bits, coset, batch)
+	const size_t t = blockIdx.x;
+	const size_t outer = t & (((size_t)1 << ps.n_outer) - 1);
+	const size_t rest = t >> ps.n_outer;
+	const int coset = (int)(rest & ((1u << P.log_rate) - 1));
+	const size_t batch = rest >> P.log_rate;
+	size_t ooff = 0;
+	for (int m = 0; m < ps.n_outer; m++) ooff |= ((outer >> m) & 1) << ps.ob[m];
+	uint32_t* dst = P.dst + (((batch << P.log_rate) + (size_t)coset) * n) * L;
+	const uint32_t* src = IN_COMPACT ? (P.src + batch * n * L) : dst;
+	auto tile_off = [&](int q) -> size_t {
+		size_t off = 0;
+#pragma unroll
+		for (int m = 0; m < kBlkBits; m++) off |= (size_t)((q >> m) & 1) << ps.bb[m];
+		return off;
+	};
+	// work-group-uniform twiddle part (outer and coset bits) of stage j, computed once per tile by
+	// lane j; a stage reads it back with v_readlane
+	uint32_t cuv = 0;
+	if (lane < ps.k) {
+		for (int m = 0; m < ps.n_outer; m++)
+			if ((outer >> m) & 1) cuv ^= ps.two[lane][m];
+		for (int b = 0; b < P.log_rate; b++)
+			if ((coset >> b) & 1) cuv ^= ps.twc[lane][b];
+	}
+	auto ucu = [&](int j) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)cuv, j); };
+
+	// ---- coalesced tile load (pieces of 16 B; block q = 32 L words) into LDS planes
+	// (plane l: block q at q * kLimbStride); HALF: blocks with tile bit 6 = h, one half at a time
+	constexpr int NH = HALF ? 2 : 1;
+	constexpr int LPH = kLoads / NH;  // loads per thread per half
+	auto issue = [&](uint4* g, int h) {
+#pragma unroll
+		for (int r = 0; r < LPH; r++) {
+			const int u = tid + r * NT;
+			const int q = h * (kTileBlocks / NH) + u / (8 * L), j = u % (8 * L);
+			g[r] = RT_DBG(1) ? make_uint4(u, j, q, tid) : ld_stream(src + (ooff | tile_off(q)) * L + 4 * j);
+		}
+	};
+	auto to_lds = [&](const uint4* g) {
+#pragma unroll
+		for (int r = 0; r < LPH; r++) {
+			const int u = tid + r * NT;
+			const int lq = u / (8 * L), j = u % (8 * L);
+			if (IN_COMPACT && L > 1) {
+				// compact element j of block q: limb l to plane l, word j
+				const uint32_t v[4] = {g[r].x, g[r].y, g[r].z, g[r].w};
+#pragma unroll
+				for (int l = 0; l < 4; l++) lds[l * PL + lq * kLimbStride + j] = v[l];
+			} else {
+				// bitsliced limb j / 8, words 4 (j % 8).. (or four compact GF(2^32) elements)
+				*(uint4*)(lds + (j >> 3) * PL + lq * kLimbStride + 4 * (j & 7)) = g[r];
+			}
+		}
+	};
+
+	const int c0 = (lane ^ (lane >> 2)) & 1, c1 = ((lane >> 1) ^ (lane >> 2)) & 1;
+	const int G = c0 | (c1 << 1) | (lane & 0x3c);  // lane coordinates c5..c0 as a number
+	const uint32_t* pl = lds + w * PL;
+	uint32_t R0[32], R1[32];
+	// initial mapping: register bit <-> tile bit 6, coordinate c_k <-> tile bit k
+	if (HALF) {
+		uint4 g0[LPH], g1[LPH];
+		issue(g0, 0);
+		issue(g1, 1);
+		to_lds(g0);
+		__syncthreads();
+#pragma unroll
+		for (int i = 0; i < 32; i += 4) rt_unpack(R0 + i, *(const uint4*)(pl + G * kLimbStride + i));
+		__syncthreads();
+		to_lds(g1);
+		__syncthreads();
+#pragma unroll
+		for (int i = 0; i < 32; i += 4) rt_unpack(R1 + i, *(const uint4*)(pl + G * kLimbStride + i));
+	} else {
+		uint4 g[kLoads];
+		issue(g, 0);
+		to_lds(g);
+		__syncthreads();
+#pragma unroll
+		for (int i = 0; i < 32; i += 4) {
+			rt_unpack(R0 + i, *(const uint4*)(pl + G * kLimbStride + i));
+			rt_unpack(R1 + i, *(const uint4*)(pl + (64 + G) * kLimbStride + i));
+		}
+	}
+	if (IN_COMPACT) {
+		transpose32(R0);
+		transpose32(R1);
+	}
+
+	// LDS parking slots of this lane (the staging planes are idle during the stages): blocks at
+	// plane slots L and 64 + L, conflict-free for ds_write_b128 / ds_read_b128
+	__syncthreads();  // every wave has read its input blocks
+	uint32_t* park = lds + w * PL + lane * kLimbStride;
+	RT_TS(1);
+
+	// ---- block stages, tile bit 6 down to mlow
+	// the bottom pass always runs all 7 block stages (mlow = 0); upper passes at least the one on
+	// tile bit 6: a compile-time lower bound keeps the loop from having a zero-trip path
+	const int mlow = LAST ? 0 : ps.mlow;
+#pragma unroll 1
+	for (int m = kBlkBits - 1; m >= mlow; m--) {
+		{
+			// partner lane L ^ pi_m and coordinate c_m = parity(L & kappa_m) (see the table above)
+			const int pi = m == 6 ? 0 : m == 5 ? 32 : m == 4 ? 16 : m == 3 ? 8 : m == 2 ? 7 : m == 1 ? 2 : 1;
+			const int kappa = m == 6 ? 0 : m == 5 ? 32 : m == 4 ? 16 : m == 3 ? 8 : m == 2 ? 4 : m == 1 ? 6 : 5;
+			const uint32_t mk = 0u - (uint32_t)(__builtin_popcount(lane & kappa) & 1);
+			rt_swap(R0, R1, mk, (lane ^ pi) << 2);
+		}
+		uint32_t tw = ucu(ps.jm[m]);
+#pragma unroll
+		for (int b = 0; b < 6; b++) tw ^= ps.tau[m][b] & (0u - (uint32_t)((lane >> b) & 1));
+		uint32_t W[32], Pr[32];
+#pragma unroll
+		for (int i = 0; i < 32; i++) W[i] = (uint32_t)__builtin_amdgcn_sbfe(tw, i, 1);
+		if (C::PARK) {
+			// R0 idles during the multiply: park it in this lane's LDS slot (32 VGPRs for the circuit)
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) *(uint4*)(park + i) = rt_pack(R0 + i);
+		}
+		// (mul_tw_packed, the packed-leaf form, needs ~40 fewer VGPRs in isolation but measured
+		// slower here: bottom pass block stages 59 k -> 77 k cycles per wave-tile)
+		__builtin_amdgcn_sched_barrier(0);
+		mul_tw<FMAX>(ps.field_m[m], R1, W, Pr);
+		__builtin_amdgcn_sched_barrier(0);
+		if (C::PARK) {
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) rt_unpack(R0 + i, *(const uint4*)(park + i));
+		}
+#pragma unroll
+		for (int i = 0; i < 32; i++) {
+			R0[i] ^= Pr[i];
+			R1[i] ^= R0[i];
+		}
+	}
+
+	RT_TS(2);
+	if (LAST) {
+		// ---- stages 4..0 inside the words. Mapping now: register bit <-> tile bit 0 (index bit 5),
+		// c_k <-> tile bit k + 1. Per stage one multiply serves both blocks: R0's v-lanes move down
+		// onto the u positions, R1's v-lanes stay.
+#pragma unroll 1
+		for (int s = 4; s >= 0; s--) {
+			const int d = 1 << s;
+			const uint32_t um = ~lane_mask(s);
+			uint32_t cb = ucu(s - ps.lo) ^ ps.cb_const[s];
+#pragma unroll
+			for (int b = 0; b < 6; b++) cb ^= ps.tau_iw[s][b] & (0u - (uint32_t)((lane >> b) & 1));
+			uint32_t W[32], T[32];
+#pragma unroll
+			for (int i = 0; i < 32; i++) {
+				T[i] = __builtin_amdgcn_bitop3_b32(R0[i] >> d, R1[i], um, 0xe4);  // (R0>>d & um) | (R1 & ~um)
+				W[i] = ps.pat[s][i] ^ (uint32_t)__builtin_amdgcn_sbfe(cb, i, 1);
+			}
+			// both blocks idle during the multiply: park them in LDS
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) {
+				*(uint4*)(park + i) = rt_pack(R0 + i);
+				*(uint4*)(park + 64 * kLimbStride + i) = rt_pack(R1 + i);
+			}
+			__builtin_amdgcn_sched_barrier(0);
+			mul_tw<FMAX>(ps.field_s[s], T, W, T);
+			__builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) {
+				rt_unpack(R0 + i, *(const uint4*)(park + i));
+				rt_unpack(R1 + i, *(const uint4*)(park + 64 * kLimbStride + i));
+			}
+#pragma unroll
+			for (int i = 0; i < 32; i++) {
+				const uint32_t a = __builtin_amdgcn_bitop3_b32(T[i], um, R0[i], 0x6a);       // R0 ^ (T & um)
+				const uint32_t b = __builtin_amdgcn_bitop3_b32(T[i] >> d, um, R1[i], 0x6a);  // R1 ^ ((T >> d) & um)
+				R0[i] = __builtin_amdgcn_bitop3_b32(a << d, um, a, 0x9a);                    // a ^ ((a << d) & ~um)
+				R1[i] = __builtin_amdgcn_bitop3_b32(b << d, um, b, 0x9a);
+			}
+		}
+		transpose32(R0);
+		transpose32(R1);
+		RT_TS(3);
+		// lane holds limb w of the 64 consecutive elements 64 G .. 64 G + 63
+		__syncthreads();  // every wave is done with its parking slots
+		uint32_t* op = lds + w * kRtOutPlane;
+#pragma unroll
+		for (int i = 0; i < 32; i += 4) {
+			*(uint4*)(op + G * 68 + i) = rt_pack(R0 + i);
+			*(uint4*)(op + G * 68 + 32 + i) = rt_pack(R1 + i);
+		}
+		__syncthreads();
+		if (L == 4) {
+			for (int e = tid; e < 4096; e += NT) {
+				const int a = e + ((e >> 6) << 2);
+				const uint4 v = make_uint4(lds[a], lds[kRtOutPlane + a], lds[2 * kRtOutPlane + a], lds[3 * kRtOutPlane + a]);
+				if (!RT_DBG(2)) st_stream(dst + (ooff | (size_t)e) * 4, v);
+			}
+		} else {
+			for (int e = 4 * tid; e < 4096; e += 4 * NT) {
+				const int a = e + ((e >> 6) << 2);
+				const uint4 v = *(const uint4*)(lds + a);
+				if (!RT_DBG(2)) st_stream(dst + (ooff | (size_t)e), v);
+			}
+		}
+	} else {
+		// final mapping: register bit <-> tile bit mlow, c_k <-> k (k < mlow) or k + 1 (k >= mlow);
+		// block R_h has tile bit mlow = h and, with that bit removed, local index G
+		auto store_half = [&](int h) {
+#pragma unroll 4
+			for (int r = 0; r < kLoads / 2; r++) {
+				const int u = tid + r * NT;
+				const int lq = u / (8 * L), j = u % (8 * L);
+				const int q = ((lq >> mlow) << (mlow + 1)) | (h << mlow) | (lq & ((1 << mlow) - 1));
+				const uint4 v = *(const uint4*)(lds + (j >> 3) * PL + (HALF ? lq : lq + 64 * h) * kLimbStride + 4 * (j & 7));
+				if (!RT_DBG(2)) st_stream(dst + (ooff | tile_off(q)) * L + 4 * j, v);
+			}
+		};
+		uint32_t* sp = lds + w * PL + G * kLimbStride;
+		__syncthreads();
+		if (HALF) {
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) *(uint4*)(sp + i) = rt_pack(R0 + i);
+			__syncthreads();
+			store_half(0);
+			__syncthreads();
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) *(uint4*)(sp + i) = rt_pack(R1 + i);
+			__syncthreads();
+			store_half(1);
+		} else {
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) {
+				*(uint4*)(sp + i) = rt_pack(R0 + i);
+				*(uint4*)(sp + 64 * kLimbStride + i) = rt_pack(R1 + i);
+			}
+			__syncthreads();
+			store_half(0);
+			store_half(1);
+		}
+		RT_TS(3);
+	}
+	RT_TS(4);
+#ifdef BN_DEV
+	if (P.trace && lane == 0) {
+		unsigned long long* o = P.trace + ((size_t)blockIdx.x * L + w) * 8;
+		o[0] = ts[1] - ts[0];  // load
+		o[1] = ts[2] - ts[1];  // block stages
+		o[2] = ts[3] - ts[2];  // in-word stages + transposes (bottom) / staging out (upper)
+		o[3] = ts[4] - ts[3];  // store
+		o[4] = 1;
+	}
+#endif
+}
+
+// lane bits that lane coordinate c_k depends on
+static const int kCoordDeps[6][2] = {{0, 2}, {1, 2}, {2, -1}, {3, -1}, {4, -1}, {5, -1}};
+
+static int make_rt(const BsPass& p, bool bottom, RtPass* out) {
+	RtPass r;
+	memset(&r, 0, sizeof r);
+	r.lo = p.lo;
+	r.k = p.k;
+	r.role = p.role;
+	r.n_outer = p.n_outer;
+	memcpy(r.bb, p.bb, sizeof r.bb);
+	memcpy(r.ob, p.ob, sizeof r.ob);
+	memcpy(r.two, p.two, sizeof r.two);
+	memcpy(r.twc, p.twc, sizeof r.twc);
+	for (int m = 0; m < kBlkBits; m++) r.jm[m] = -1;
+	for (int j = 0; j < p.k; j++)
+		if (p.stage_m[j] >= 0) {
+			r.jm[p.stage_m[j]] = j;
+			r.field_m[p.stage_m[j]] = p.field[j];
+		}
+	r.mlow = kBlkBits;
+	for (int m = 0; m < kBlkBits; m++)
+		if (r.jm[m] >= 0) r.mlow = std::min(r.mlow, m);
+	// the stage bits must be the top tile bits (stages run from tile bit 6 down)
+	for (int m = r.mlow; m < kBlkBits; m++)
+		if (r.jm[m] < 0) return BN_ERR_UNSUPPORTED;
+	if (bottom && r.mlow != 0) return BN_ERR_UNSUPPORTED;
+	auto add_coords = [&](uint32_t* tau, int kmin, const uint32_t* twt) {
+		for (int k = kmin; k < 6; k++)
+			for (int b : kCoordDeps[k])
+				if (b >= 0) tau[b] ^= twt[k + 1];
+	};
+	for (int m = r.mlow; m < kBlkBits; m++) add_coords(r.tau[m], m, p.twt[r.jm[m]]);
+	if (bottom) {
+		for (int s = 0; s < 5; s++) {
+			const int j = s - p.lo;
+			r.field_s[s] = p.field[j];
+			r.cb_const[s] = p.twt[j][0];
+			add_coords(r.tau_iw[s], 0, p.twt[j]);
+			for (int i = 0; i < 32; i++) {
+				// p.pat folds the variant-1 block difference (tile bit 6); fold tile bit 0 instead
+				uint32_t v = p.pat[s][i];
+				if ((p.twt[j][kBlkBits - 1] >> i) & 1) v ^= ~lane_mask(s);
+				if ((p.twt[j][0] >> i) & 1) v ^= ~lane_mask(s);
+				r.pat[s][i] = v;
+			}
+		}
+	}
+	*out = r;
+	return BN_OK;
+}
+
+template <int L, int FMAX>
+static const void* rt_kernel_f(int role) {
+	switch (role) {
+		case ROLE_FIRST: return (const void*)antt_rt_pass<L, ROLE_FIRST, FMAX>;
+		case ROLE_MID: return (const void*)antt_rt_pass<L, ROLE_MID, FMAX>;
+		case ROLE_LAST: return (const void*)antt_rt_pass<L, ROLE_LAST, FMAX>;
+		default: return (const void*)antt_rt_pass<L, ROLE_SINGLE, FMAX>;
+	}
+}
+static const void* rt_kernel(int L, int role, int fmax) {
+	if (L == 4) return fmax <= 8 ? rt_kernel_f<4, 8>(role) : fmax <= 16 ? rt_kernel_f<4, 16>(role) : rt_kernel_f<4, 32>(role);
+	return fmax <= 8 ? rt_kernel_f<1, 8>(role) : fmax <= 16 ? rt_kernel_f<1, 16>(role) : rt_kernel_f<1, 32>(role);
+}
+static size_t rt_lds_bytes(int L, int role, int fmax) {
+	const bool last = role == ROLE_LAST || role == ROLE_SINGLE;
+	const int plane = (!last && fmax <= 8) ? RtCfg<ROLE_MID, 8>::PLANE : kRtPlane;
+	return (size_t)L * plane * sizeof(uint32_t);
+}
+
+static int rt_prepare() {
+	for (int L : {1, 4})
+		for (int role = 0; role < 4; role++)
+			for (int f : {8, 16, 32})
+				BN_HIP(hipFuncSetAttribute(rt_kernel(L, role, f), hipFuncAttributeMaxDynamicSharedMemorySize,
+				                           (int)rt_lds_bytes(L, role, f)));
+	return BN_OK;
+}
+
+static int launch_rt(bn_antt_plan* plan, const BsPass& pass, int i, const uint32_t* d_in, uint32_t* d_out, size_t batch,
+                     hipStream_t st, const BsDevKnobs& kn) {
+	const int L = plan->limbs;
+	RtParams prm;
+	prm.src = d_in;
+	prm.dst = d_out;
+	prm.log_h = plan->log_h;
+	prm.log_rate = plan->log_rate;
+	prm.trace = nullptr;
+	prm.dbg = kn.dbg;
+	const bool bottom = pass.role == ROLE_LAST || pass.role == ROLE_SINGLE;
+	int rc = make_rt(pass, bottom, &prm.p);
+	if (rc != BN_OK) BN_FAIL(rc, "register-tile pass table: stage bits are not the top tile bits");
+	const size_t ntiles = (batch << plan->log_rate) << pass.n_outer;
+	static unsigned long long* trbuf = nullptr;
+	if (kn.trace) {
+		if (!trbuf) BN_HIP(hipMalloc(&trbuf, (size_t)1 << 26));
+		BN_HIP(hipMemset(trbuf, 0, ntiles * L * 8 * 8));
+		prm.trace = trbuf;
+	}
+	rc = timing_begin(plan, i, st);
+	if (rc != BN_OK) return rc;
+	void* args[] = {&prm};
+	const int fmax = pass_fmax(pass);
+	BN_HIP(hipLaunchKernel(rt_kernel(L, pass.role, fmax), dim3((unsigned)ntiles), dim3(64 * L), args, rt_lds_bytes(L, pass.role, fmax), st));
+	rc = timing_end(plan, i, st);
+	if (rc != BN_OK) return rc;
+	if (prm.trace) {
+		const size_t g = ntiles * (size_t)L;
+		std::vector<unsigned long long> h(g * 8);
+		BN_HIP(hipStreamSynchronize(st));
+		BN_HIP(hipMemcpy(h.data(), prm.trace, g * 8 * 8, hipMemcpyDeviceToHost));
+		double acc[8] = {0};
+		for (size_t w = 0; w < g; w++)
+			for (int k = 0; k < 8; k++) acc[k] += (double)h[w * 8 + k];
+		const double t = acc[4] > 0 ? acc[4] : 1;
+		fprintf(stderr, "trace rt pass %d (fmax %d, %zu wave-tiles, cycles per wave-tile): load %.0f  block %.0f  inword/stage-out %.0f  store %.0f\n",
+		        i, fmax, (size_t)acc[4], acc[0] / t, acc[1] / t, acc[2] / t, acc[3] / t);
 	}
 	return BN_OK;
 }

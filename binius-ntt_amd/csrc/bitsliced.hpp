@@ -22,8 +22,8 @@ __device__ __forceinline__ void transpose32(uint32_t* a) {
 						 : lj == 1 ? 0x33333333u
 								   : 0x55555555u;
 #pragma unroll
-		for (int k = 0; k < 32; k++) {
-			if (k & j) continue;
+		for (int kk = 0; kk < 16; kk++) {
+			const int k = ((kk & ~(j - 1)) << 1) | (kk & (j - 1));  // the 16 words with bit lj clear
 			const uint32_t t = ((a[k] >> j) ^ a[k + j]) & m;
 			a[k] ^= t << j;
 			a[k + j] ^= t;

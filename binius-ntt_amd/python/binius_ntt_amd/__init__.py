@@ -273,7 +273,8 @@ class AdditiveNTT:
         return v.value
 
     def set_variant(self, variant):
-        """0: compact tiles, per-butterfly twiddles; 1: bitsliced tiles (default for log_h >= 12)."""
+        """0: compact tiles, per-butterfly twiddles; 1: bitsliced LDS tiles; 2: bitsliced register tiles
+        (default for log_h >= 12)."""
         _check(lib().bn_antt_plan_set_variant(self._plan, variant))
 
     def set_event_timing(self, enable):
