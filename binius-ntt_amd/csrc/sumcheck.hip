@@ -194,6 +194,7 @@ struct ScArgs {
 	int h;              // element distance of a pair inside the batch (small modes)
 	int mode;           // 0 big, 1 in-batch pairs, 2 single element (cur == 1)
 	int kmax;           // points 0..kmax
+	int skip1;          // point 1 is not computed (the host derives it from the round claim)
 	uint32_t r[4];      // fold challenge
 	uint32_t* acc;      // (kmax + 1) x 4 words, XOR-accumulated (this round's set)
 	uint32_t* clr;      // the other accumulator set: cleared here for the next round
@@ -242,10 +243,11 @@ __global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
 	// previous round's copy (ordered before this launch), so no memset is queued per round
 	if (blockIdx.x == 0 && threadIdx.x < 4 * (kMaxD + 1)) A.clr[threadIdx.x] = 0;
 	__syncthreads();
-	const int npts = A.kmax + 1;
+	const int npts = A.kmax + 1 - A.skip1;
 	const size_t item = (size_t)blockIdx.x * kQuadsPerWG + qw;
 	const size_t p = item / npts;
-	const int k = (int)(item % npts);
+	const int ki = (int)(item % npts);
+	const int k = (A.skip1 && ki >= 1) ? ki + 1 : ki;
 	if (p < A.n_pairs) {
 		uint32_t emask = 0;
 		for (int j = 0; j < A.d; j++) {
@@ -273,7 +275,7 @@ __global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
 		if (acc) atomicXor(accL + 4 * k + l, acc);  // LDS atomic
 	}
 	__syncthreads();
-	if (threadIdx.x < 4 * npts && accL[threadIdx.x]) atomicXor(A.acc + threadIdx.x, accL[threadIdx.x]);
+	if (threadIdx.x < 4 * (A.kmax + 1) && accL[threadIdx.x]) atomicXor(A.acc + threadIdx.x, accL[threadIdx.x]);
 }
 
 template <int MODE>
@@ -338,6 +340,12 @@ struct bn_sumcheck {
 	uint32_t* h_acc = nullptr;  // pinned host copy of acc (round messages)
 	hipStream_t stream = nullptr;
 	bool sharded_used = false;
+	// Round claim: once round i's points are known, move_to_next_round(r) interpolates them at r,
+	// which is this prover's sum for round i + 1 (p_i(r) = sum_x prod_j f_j'(x), per shard too).
+	// Round i + 1 then skips point 1 (p(1) = claim + p(0)): (d - 1) fewer products per pair.
+	bool have_pts = false, have_claim = false;
+	uint32_t last_pts[4 * (bn::kMaxD + 1)];
+	uint32_t claim[4];
 };
 
 namespace {
@@ -364,13 +372,14 @@ int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 		A.n_pairs = 1;
 		A.kmax = 0;
 	}
+	A.skip1 = (!fold && sc->have_claim && A.mode != 2) ? 1 : 0;
 	A.acc = sc->acc + 4 * (kMaxD + 1) * sc->par;
 	A.clr = sc->acc + 4 * (kMaxD + 1) * (1 - sc->par);
 	if (fold) memcpy(A.r, r, 16);
 	for (int k = 0; k <= kMaxD; k++)
 		for (int a = 0; a < 4; a++) A.kcol[k][a] = (uint32_t)tw_mul((uint64_t)k, 1ull << a, 2);
 	// one item per quad: fold (column, pair), messages (pair, point)
-	const size_t items = fold ? (size_t)sc->d * A.n_pairs : A.n_pairs * (size_t)(A.kmax + 1);
+	const size_t items = fold ? (size_t)sc->d * A.n_pairs : A.n_pairs * (size_t)(A.kmax + 1 - A.skip1);
 	const size_t grid = (items + kQuadsPerWG - 1) / kQuadsPerWG;
 	void* args[] = {&A};
 	const void* fns[2][3] = {{(const void*)sc_messages<0>, (const void*)sc_messages<1>, (const void*)sc_messages<2>},
@@ -634,6 +643,7 @@ extern "C" int bn_sumcheck_import_gathered(bn_sumcheck* sc, const uint32_t* word
 	sc->cur = (size_t)32 * world;
 	sc->rank = 0;
 	sc->world = 1;
+	sc->have_pts = sc->have_claim = false;  // the shards' claims are partial: recompute point 1
 	return BN_OK;
 }
 
@@ -652,10 +662,20 @@ extern "C" int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32
 	if (sc->cur == 1) {
 		memcpy(sum, acc, 16);  // mode 2 computed prod_j f_j(0) as "point 0"
 		memset(points, 0, sizeof(uint32_t) * 4 * npts);
+		sc->have_pts = false;
 	} else {
 		memcpy(points, acc, sizeof(uint32_t) * 4 * npts);
-		for (int i = 0; i < 4; i++) sum[i] = acc[i] ^ acc[4 + i];
+		if (sc->have_claim) {
+			// point 1 was skipped: p(1) = claim + p(0)
+			for (int i = 0; i < 4; i++) points[4 + i] = sc->claim[i] ^ acc[i];
+			memcpy(sum, sc->claim, 16);
+		} else {
+			for (int i = 0; i < 4; i++) sum[i] = acc[i] ^ acc[4 + i];
+		}
+		memcpy(sc->last_pts, points, sizeof(uint32_t) * 4 * npts);
+		sc->have_pts = true;
 	}
+	sc->have_claim = false;
 	sc->sharded_used = true;
 	return BN_OK;
 }
@@ -668,6 +688,12 @@ extern "C" int bn_sumcheck_move_to_next_round(bn_sumcheck* sc, const uint32_t* c
 	int rc = sc_launch(sc, true, challenge);
 	if (rc != BN_OK) return rc;
 	// no sync: the fold is ordered before the next round's messages on the prover's stream
+	if (sc->have_pts) {
+		rc = bn_sumcheck_interpolate(sc->last_pts, sc->d + 1, challenge, sc->claim);
+		if (rc != BN_OK) return rc;
+		sc->have_claim = true;
+		sc->have_pts = false;
+	}
 	sc->cur /= 2;
 	sc->round++;
 	sc->sharded_used = true;
@@ -734,15 +760,18 @@ extern "C" int bn_sumcheck_interpolate(const uint32_t* points, int num_points, c
 		return bn::u128p{(uint64_t)w[0] | ((uint64_t)w[1] << 32), (uint64_t)w[2] | ((uint64_t)w[3] << 32)};
 	};
 	const bn::u128p r = ld(challenge);
+	// (r - j) for every node j, and the node weights prod_{j != i} 1 / (i - j), which lie in GF(2^4)
+	// (inverse_at_interpolation_point, tower_7_mul.cu:22-24)
+	bn::u128p rj[16];
+	for (int j = 0; j < num_points; j++) rj[j] = bn::u128p{r.lo ^ (uint64_t)j, r.hi};
 	bn::u128p acc{0, 0};
 	for (int i = 0; i < num_points; i++) {
-		bn::u128p t = ld(points + 4 * i);
-		for (int j = 0; j < num_points; j++) {
-			if (j == i) continue;
-			t = bn::tw_mul128(t, bn::u128p{r.lo ^ (uint64_t)j, r.hi});
-			// 1 / (i - j) lies in GF(2^4) (inverse_at_interpolation_point, tower_7_mul.cu:22-24)
-			t = bn::tw_mul128(t, bn::u128p{bn::tw_inv((uint64_t)(i ^ j), 2), 0});
-		}
+		uint64_t wgt = 1;
+		for (int j = 0; j < num_points; j++)
+			if (j != i) wgt = bn::tw_mul(wgt, bn::tw_inv((uint64_t)(i ^ j), 2), 2);
+		bn::u128p t = bn::tw_mul128_host(ld(points + 4 * i), bn::u128p{wgt, 0});
+		for (int j = 0; j < num_points; j++)
+			if (j != i) t = bn::tw_mul128_host(t, rj[j]);
 		acc.lo ^= t.lo;
 		acc.hi ^= t.hi;
 	}

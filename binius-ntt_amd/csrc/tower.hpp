@@ -60,4 +60,33 @@ __host__ __device__ inline u128p tw_mul128(u128p a, u128p b) {
 	return u128p{z0 ^ z2, z1 ^ tw_mul_alpha(z2, 6)};
 }
 
+// Host-only fast path (round claims, interpolation): the Karatsuba recursion stops at GF(2^8),
+// whose products come from a 64 KiB table (built on first use), so a GF(2^128) product is 27
+// lookups per GF(2^64) sub-product instead of 729 GF(2) leaves.
+__host__ inline const uint8_t* tw_mul8_table() {
+	static uint8_t* t = [] {
+		static uint8_t tab[256 * 256];
+		for (int a = 0; a < 256; a++)
+			for (int b = 0; b < 256; b++) tab[a * 256 + b] = (uint8_t)tw_mul((uint64_t)a, (uint64_t)b, 3);
+		return tab;
+	}();
+	return t;
+}
+__host__ inline uint64_t tw_mul_host(uint64_t a, uint64_t b, int h) {
+	if (h <= 3) return tw_mul8_table()[(a & 0xff) * 256 + (b & 0xff)];
+	const int half = 1 << (h - 1);
+	const uint64_t m = half >= 64 ? ~0ull : ((1ull << half) - 1);
+	const uint64_t a0 = a & m, a1 = (a >> half) & m, b0 = b & m, b1 = (b >> half) & m;
+	const uint64_t z0 = tw_mul_host(a0, b0, h - 1);
+	const uint64_t z2 = tw_mul_host(a1, b1, h - 1);
+	const uint64_t z1 = tw_mul_host(a0 ^ a1, b0 ^ b1, h - 1) ^ z0 ^ z2;
+	return (z0 ^ z2) | ((z1 ^ tw_mul_alpha(z2, h - 1)) << half);
+}
+__host__ inline u128p tw_mul128_host(u128p a, u128p b) {
+	const uint64_t z0 = tw_mul_host(a.lo, b.lo, 6);
+	const uint64_t z2 = tw_mul_host(a.hi, b.hi, 6);
+	const uint64_t z1 = tw_mul_host(a.lo ^ a.hi, b.lo ^ b.hi, 6) ^ z0 ^ z2;
+	return u128p{z0 ^ z2, z1 ^ tw_mul_alpha(z2, 6)};
+}
+
 }  // namespace bn

@@ -382,11 +382,17 @@ class LutEmitter:
                     raise AssertionError("LUT mapping differs from the DAG")
 
 
-EMITTER = os.environ.get("BN_GEN_EMITTER", "lut")
+EMITTER = os.environ.get("BN_GEN_EMITTER", "auto")
 
 
-def make_emitter(dag, roots):
-    return LutEmitter(dag, roots) if EMITTER == "lut" else Emitter(dag, roots)
+def make_emitter(dag, roots, low_pressure=False):
+    """auto: XOR3 / AND-XOR fusion (Emitter) for the circuits that run inside register-hungry
+    kernels (the full GF(2^8..2^32) multiplies of the NTT passes and the sumcheck's quad product:
+    the LUT cover re-derives nodes and reorders, and there it costs more in spills than it saves in
+    gates — c4 d=3 4.5 -> 6.0 ms measured), the LUT mapping everywhere else."""
+    if EMITTER == "lut" or (EMITTER == "auto" and not low_pressure):
+        return LutEmitter(dag, roots)
+    return Emitter(dag, roots)
 
 
 def count_ops(lines):
@@ -536,7 +542,7 @@ def gen_full(h, accumulate=False):
         acc = [d.inp("o%d" % i) for i in range(n)]
         imap.update({"o%d" % i: "o%d_" % i for i in range(n)})
         res = [d.xor(r, q) for r, q in zip(res, acc)]
-    e = make_emitter(d, res)
+    e = make_emitter(d, res, low_pressure=h <= 5)
     body = e.emit(imap, [("out[%d]" % i, res[i]) for i in range(n)], BARRIER_EVERY if h <= 5 else 0)
     pre = ["const uint32_t a%d_ = a[%d];" % (i, i) for i in range(n)]
     pre += ["const uint32_t b%d_ = b[%d];" % (i, i) for i in range(n)]
