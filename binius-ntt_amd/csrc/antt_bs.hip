@@ -762,7 +762,7 @@ struct RtCfg {
 	static constexpr bool LAST = ROLE == ROLE_LAST || ROLE == ROLE_SINGLE;
 	static constexpr bool HALF = !LAST && FMAX <= 8;
 	static constexpr int OCC = HALF ? 3 : 2;
-	static constexpr bool PARK = true;  // idle blocks wait in LDS during the multiplies (register pressure)
+	static constexpr bool PARK = FMAX > 8;  // idle blocks wait in LDS during the GF(2^16/32) multiplies (register pressure)
 	static constexpr int PLANE = HALF ? (kTileBlocks / 2) * kLimbStride + 32 : kRtPlane;
 };
 

@@ -496,6 +496,19 @@ extern "C" int bn_sumcheck_create_device(int device, int num_vars, int d, int tr
 		sc_free(sc);
 		return rc;
 	}
+	{
+		// order the prover's stream after the work already queued on the legacy default stream
+		// (producers on other streams must still complete first: see the header)
+		hipEvent_t ready = nullptr;
+		hipError_t e = hipEventCreateWithFlags(&ready, hipEventDisableTiming);
+		if (e == hipSuccess) e = hipEventRecord(ready, 0);
+		if (e == hipSuccess) e = hipStreamWaitEvent(sc->stream, ready, 0);
+		if (ready) (void)hipEventDestroy(ready);
+		if (e != hipSuccess) {
+			sc_free(sc);
+			BN_FAIL(BN_ERR_HIP, "ordering after the default stream: %s", hipGetErrorString(e));
+		}
+	}
 	if (take && in_words >= 128) {
 		sc->cols = (uint32_t*)d_evals;
 		sc->col_words = in_words;

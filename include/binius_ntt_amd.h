@@ -156,9 +156,9 @@ int bn_sumcheck_create(int device, int num_vars, int composition_size, int data_
 /* As above but from device memory already holding the columns (no host copy). The buffer
  * is copied into the prover's own storage unless take_ownership != 0, in which case the
  * prover folds it in place and frees it with hipFree on destroy (so it must come from
- * hipMalloc). Precondition: the columns are complete when this is called (the copy runs on
- * the prover's own stream, unordered with the caller's streams); the Python mirror
- * synchronises the current stream first. */
+ * hipMalloc). The copy (or first use) runs on the prover's own stream, ordered after the work
+ * queued on the legacy default stream; a producer on any other stream must have completed
+ * (the Python mirror synchronises the tensor's current stream first). */
 int bn_sumcheck_create_device(int device, int num_vars, int composition_size, int data_is_transposed,
                               void* d_evals, int take_ownership, bn_sumcheck** sc);
 /* Replaces Sumcheck::this_round_messages(sum, points) (sumcheck.cuh:130-246):

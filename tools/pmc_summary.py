@@ -63,5 +63,38 @@ def main():
             print("traffic per launch of %s: %.4g B" % (dom[0], cur[traffic_log_h]))
 
 
+def headline(root, log_h, out_dir):
+    """Per-pass counters of the headline transform (kernel variant 1: antt_bs_pass<4, ROLE, ...>;
+    with three passes ROLE 0/1/2 = pass 0/1/2) -> out_dir/pmc_summary.json and pmc_traffic.json,
+    keyed "log_h=N" -> pass index, as bench.py reads them."""
+    with open(os.path.join(root, "pmc_summary.json")) as f:
+        summ = json.load(f)
+    per_pass, traffic = {}, {}
+    for k, m in summ.items():
+        if "antt_bs_pass<4, " not in k:
+            continue
+        role = int(k.split("antt_bs_pass<4, ")[1].split(",")[0])
+        per_pass[str(role)] = dict(m, kernel=k)
+        if "HBM_READ_BYTES_corrected" in m and "HBM_WRITE_BYTES" in m:
+            traffic[str(role)] = m["HBM_READ_BYTES_corrected"] + m["HBM_WRITE_BYTES"]
+    key = "log_h=%d" % log_h
+    for name, data in (("pmc_summary.json", per_pass), ("pmc_traffic.json", traffic)):
+        path = os.path.join(out_dir, name)
+        cur = json.load(open(path)) if os.path.exists(path) else {}
+        cur[key] = data
+        with open(path, "w") as f:
+            json.dump(cur, f, indent=1)
+    print("headline %s: passes %s, traffic %s" % (key, sorted(per_pass), traffic))
+
+
 if __name__ == "__main__":
-    main()
+    # --headline LOG_H OUT_DIR [ROOT]: summarise ROOT's pmc_* runs, then write the per-pass files
+    if "--headline" in sys.argv:
+        i = sys.argv.index("--headline")
+        log_h, out_dir = int(sys.argv[i + 1]), sys.argv[i + 2]
+        rest = sys.argv[1:i] + sys.argv[i + 3:]
+        sys.argv = [sys.argv[0]] + rest
+        main()
+        headline(rest[0] if rest else os.path.join(ROOT, "gpurun_out"), log_h, out_dir)
+    else:
+        main()
