@@ -151,6 +151,10 @@ def load_traffic(log_h):
 def main():
     a = parse()
     relaunch_if_needed(a)
+    # stdout carries exactly one JSON line (rank 0): library chatter (e.g. gloo's connection
+    # messages on std::cout) is sent to stderr by pointing fd 1 there for the rest of the run
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -368,7 +372,8 @@ def main():
         if world == 1:
             res["apply_e2e"] = apply_e2e(B, ntt, n)
         res["cpu_baseline"] = cpu_baseline() if (not a.no_cpu and world == 1) else None
-        print(json.dumps(res))
+        json_out.write(json.dumps(res) + "\n")
+        json_out.flush()
     if world > 1:
         dist.destroy_process_group()
 
