@@ -78,7 +78,10 @@ int bn_antt_plan_query(const bn_antt_plan* plan, int what, int64_t* value);
 /* Kernel selection, the analogue of choosing AdditiveNTT vs ModifiedAdditiveNTT
  * (src/ulvt/ntt/modified_antt.cuh:223-427, benchmark_antt.cu): 0 = compact tiles with the twiddle
  * recomputed per butterfly from the subspace table (the reference kernel's scheme), 1 = bitsliced
- * tiles with host-tabulated twiddle contributions (default when log_h >= 12). */
+ * tiles with host-tabulated twiddle contributions (default when log_h >= 12), 2 = the same
+ * passes with register-resident tiles (lane-to-lane exchanges instead of LDS stages; measured
+ * slower than 1 except for GF(2^8)-only passes). Variants 1 and 2 need
+ * log_h >= 12; results are identical. */
 int bn_antt_plan_set_variant(bn_antt_plan* plan, int variant);
 
 /* Profiling hook for bench.py: records hipEvents around every kernel launch of the next

@@ -166,3 +166,26 @@ def test_full_protocol_with_gpu_verifier(dev):
     assert np.array_equal(s, claim)
     assert np.array_equal(B.evaluate_multilinear_composition(bs, n, d, True, ch), claim)
     sc.close()
+
+
+@pytest.mark.parametrize("n,d", [(9, 3), (7, 2), (8, 4)])
+def test_point1_from_claim_irregular_call_patterns(n, d, dev):
+    """Rounds after a messages call skip point 1 (p(1) = claim + p(0), sumcheck.hip round claims).
+    A round whose messages were never asked for, and a second messages call in one round, must
+    fall back to computing every point: the transcript of the rounds that are asked still matches
+    the oracle's word for word."""
+    ev, ch = _case(n, d, 4242 + n + d)
+    bs = O.bitslice128(ev)
+    want_s, want_p = O.sumcheck_run(bs, n, d, 1, ch)
+    sc = B.Sumcheck(n, d, True, bs)
+    for r in range(n + 1):
+        if r % 3 != 1:  # rounds 1, 4, 7, ... are folded without their messages
+            s, p = sc.this_round_messages()
+            assert np.array_equal(s, want_s[r]), "round %d sum" % r
+            assert np.array_equal(p, want_p[r]), "round %d points" % r
+            if r % 3 == 2:  # and some rounds are asked twice
+                s2, p2 = sc.this_round_messages()
+                assert np.array_equal(s2, want_s[r]) and np.array_equal(p2, want_p[r]), "round %d repeat" % r
+        if r < n:
+            sc.move_to_next_round(ch[r])
+    sc.close()
