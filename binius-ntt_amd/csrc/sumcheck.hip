@@ -701,6 +701,7 @@ extern "C" int bn_sumcheck_move_to_next_round(bn_sumcheck* sc, const uint32_t* c
 	int rc = sc_launch(sc, true, challenge);
 	if (rc != BN_OK) return rc;
 	// no sync: the fold is ordered before the next round's messages on the prover's stream
+	sc->have_claim = false;  // a claim not consumed by this round's messages is stale now
 	if (sc->have_pts) {
 		rc = bn_sumcheck_interpolate(sc->last_pts, sc->d + 1, challenge, sc->claim);
 		if (rc != BN_OK) return rc;
