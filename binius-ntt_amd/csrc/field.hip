@@ -6,6 +6,7 @@
 #include "common.hpp"
 #include "field_dev.hpp"
 #include "bitsliced.hpp"
+#include "quad_mul.hpp"
 
 namespace bn {
 
@@ -85,6 +86,29 @@ __global__ __launch_bounds__(256) void k_repeat_bitsliced(uint32_t* state, const
 	for (int i = 0; i < 128; i++) state[128 * t + i] = x[i];
 }
 
+// kind 2: the same bitsliced repeat loop on the sumcheck's quad-lane product (quad_mul.hpp): block
+// b's 128 words are spread over the 4 lanes of quad b (lane l holds limb l), operands and partial
+// products go through the quad's LDS slot, so no lane holds more than ~4 x 32 words of field data.
+__global__ __launch_bounds__(256, 2) void k_repeat_quad(uint32_t* state, const uint32_t* operand, size_t blocks, int iters) {
+	extern __shared__ uint32_t lds[];
+	const int l = threadIdx.x & 3, qw = threadIdx.x >> 2;
+	const quad::Slot S{lds + qw * quad::kQuadWords};
+	const size_t b = (size_t)blockIdx.x * 64 + qw;
+	if (b >= blocks) return;  // whole quads leave together (b is uniform per quad)
+	uint32_t x[32], y[32];
+	quad::ld32(x, state + 128 * b + 32 * l);
+	quad::ld32(y, operand + 128 * b + 32 * l);
+	quad::sst(S, l, x);
+	for (int it = 0; it < iters; it++) {
+		quad::sst(S, 4 + l, y);
+		quad::quad_mul<false>(S, nullptr, l);  // row l <- (rows 0..3) * (rows 4..7)
+	}
+	quad::wsync();
+	quad::sld(x, S, l);
+	quad::st32(state + 128 * b + 32 * l, x);
+}
+static size_t quad_lds_bytes() { return (size_t)64 * quad::kQuadWords * sizeof(uint32_t); }
+
 static unsigned grid_for(size_t n, unsigned block) {
 	size_t g = (n + block - 1) / block;
 	if (g > 65535u * 16u) g = 65535u * 16u;
@@ -134,11 +158,20 @@ extern "C" int bn_gf128_mul_bitsliced_device(const void* a, const void* b, void*
 extern "C" int bn_gf128_mul_repeat_device(int kind, void* state, const void* operand, size_t threads, int iters,
 										  void* stream) {
 	BN_CHECK_ARG(state && operand, "NULL device pointer");
-	BN_CHECK_ARG(kind == 0 || kind == 1, "kind must be 0 (compact) or 1 (bitsliced)");
+	BN_CHECK_ARG(kind >= 0 && kind <= 2, "kind must be 0 (compact), 1 (bitsliced) or 2 (bitsliced, quad-lane product)");
 	BN_CHECK_ARG(iters >= 0, "iters must be >= 0");
 	if (!threads) return BN_OK;
 	const unsigned grid = (unsigned)((threads + 255) / 256);
-	if (kind == 0)
+	if (kind == 2) {
+		static bool attr = false;
+		if (!attr) {
+			BN_HIP(hipFuncSetAttribute((const void*)k_repeat_quad, hipFuncAttributeMaxDynamicSharedMemorySize,
+			                           (int)quad_lds_bytes()));
+			attr = true;
+		}
+		hipLaunchKernelGGL(k_repeat_quad, dim3((unsigned)((threads + 63) / 64)), dim3(256), quad_lds_bytes(),
+		                   (hipStream_t)stream, (uint32_t*)state, (const uint32_t*)operand, threads, iters);
+	} else if (kind == 0)
 		hipLaunchKernelGGL(k_repeat_compact, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint4*)state,
 						   (const uint4*)operand, threads, iters);
 	else

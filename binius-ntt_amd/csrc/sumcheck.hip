@@ -29,6 +29,7 @@
 
 #include "bitsliced.hpp"
 #include "common.hpp"
+#include "quad_mul.hpp"
 #include "tower.hpp"
 
 namespace bn {
@@ -36,129 +37,7 @@ namespace {
 
 constexpr int kScThreads = 256;
 constexpr int kQuadsPerWG = kScThreads / 4;
-constexpr int kRowWords = 36;    // LDS words per 32-word row (padding: bank spread)
-constexpr int kQuadWords = 304;  // LDS words per quad slot (8 padded rows + spread)
-constexpr int kMaxD = 8;
-
-// compiler ordering for LDS traffic between lanes of one wave (the hardware executes a wave's
-// LDS instructions in order)
-__device__ __forceinline__ void wsync() {
-	asm volatile("" ::: "memory");
-	__builtin_amdgcn_wave_barrier();
-}
-
-__device__ __forceinline__ void ld32(uint32_t* r, const uint32_t* p) {
-#pragma unroll
-	for (int i = 0; i < 32; i += 4) *(uint4*)(r + i) = *(const uint4*)(p + i);
-}
-__device__ __forceinline__ void st32(uint32_t* p, const uint32_t* r) {
-#pragma unroll
-	for (int i = 0; i < 32; i += 4) *(uint4*)(p + i) = *(const uint4*)(r + i);
-}
-
-// bitsliced multiply_alpha on GF(2^(2^H)) (binary_tower.cuh multiply_alpha): out may not alias a
-template <int H>
-__device__ __forceinline__ void bs_alpha(const uint32_t* a, uint32_t* out) {
-	if constexpr (H == 0) {
-		out[0] = a[0];
-	} else {
-		constexpr int half = 1 << (H - 1);
-		uint32_t t[half];
-		bs_alpha<H - 1>(a + half, t);
-#pragma unroll
-		for (int i = 0; i < half; i++) {
-			out[i] = a[half + i];
-			out[half + i] = a[i] ^ t[i];
-		}
-	}
-}
-
-// A quad's LDS slot: 8 rows of 32 words, rows padded to 36 words and slots to 304 words. With
-// that padding the access patterns of quad_mul (operand rows l and 4+l, product rows 2l and
-// 2l+1, the cross-lane reads) are nearly free of bank conflicts for both the 16-lane
-// ds_read_b128 groups and the 8-lane ds_write_b128 groups (3328 -> 192 extra cycles per product
-// in a lane-group model), while every address stays a base plus an immediate offset.
-struct Slot {
-	uint32_t* base;
-	__device__ __forceinline__ uint32_t* row(int r) const { return base + kRowWords * r; }
-};
-__device__ __forceinline__ void sld(uint32_t* x, const Slot& S, int r) { ld32(x, S.row(r)); }
-__device__ __forceinline__ void sst(const Slot& S, int r, const uint32_t* x) { st32(S.row(r), x); }
-
-// GF(2^128) product on a quad. On entry slot row l holds limb l of the first operand and row 4+l
-// limb l of the second — or, with B_SHARED, the second operand is the unswizzled 128-word B
-// shared by every quad (the fold's broadcast challenge). On exit row l holds limb l of the product.
-template <bool B_SHARED>
-__device__ __forceinline__ void quad_mul(const Slot& S, const uint32_t* B, int l) {
-	wsync();
-	const int ia = l & 1, jb = (l == 1 || l == 2) ? 1 : 0;
-	const int ra = 2 * ia, rb = 4 + 2 * jb;  // rows of a0 (a1 = ra + 1) and b0 (b1 = rb + 1)
-	auto ldb = [&](uint32_t* x, int h) {
-		if constexpr (B_SHARED)
-			ld32(x, B + 64 * jb + 32 * h);
-		else
-			sld(x, S, rb + h);
-	};
-	uint32_t x[32], y[32], z[32];
-	// GF(2^64) Karatsuba: z0 = a0 b0, z2 = a1 b1, z1 = (a0+a1)(b0+b1) + z0 + z2; at most one
-	// 32-word value is live across a circuit (the circuits themselves need ~160 VGPRs), the
-	// rest is parked in the quad's LDS slot once the operands have been consumed.
-	sld(x, S, ra);
-	ldb(y, 0);
-	bsm5_mul(x, y, z);  // z0
-	__builtin_amdgcn_sched_barrier(0);
-	wsync();  // also a compiler memory barrier: operands are re-read, never kept live
-	sld(x, S, ra + 1);
-	ldb(y, 1);
-	bsm5_mul(x, y, y);  // z2
-	__builtin_amdgcn_sched_barrier(0);
-	wsync();
-#pragma unroll
-	for (int i = 0; i < 32; i++) z[i] ^= y[i];  // lo = z0 + z2
-	bs_alpha<5>(y, x);
-#pragma unroll
-	for (int i = 0; i < 32; i++) y[i] = z[i] ^ x[i];  // lo + alpha(z2)
-	uint32_t sa[32], sb[32];
-	{
-		const uint32_t* A0 = S.row(ra);
-		const uint32_t* B0 = B_SHARED ? B + 64 * jb : S.row(rb);
-		const int bstep = B_SHARED ? 32 : kRowWords;
-#pragma unroll
-		for (int i = 0; i < 32; i += 4) {
-			const uint4 p = *(const uint4*)(A0 + i), q = *(const uint4*)(A0 + kRowWords + i);
-			const uint4 u = *(const uint4*)(B0 + i), v = *(const uint4*)(B0 + bstep + i);
-			sa[i] = p.x ^ q.x, sa[i + 1] = p.y ^ q.y, sa[i + 2] = p.z ^ q.z, sa[i + 3] = p.w ^ q.w;
-			sb[i] = u.x ^ v.x, sb[i + 1] = u.y ^ v.y, sb[i + 2] = u.z ^ v.z, sb[i + 3] = u.w ^ v.w;
-		}
-	}
-	wsync();  // every lane of the quad has read its operands: the slot is free
-	sst(S, 2 * l, z);
-	sst(S, 2 * l + 1, y);
-	__builtin_amdgcn_sched_barrier(0);
-	bsm5_mul(sa, sb, x);  // (a0+a1)(b0+b1)
-	__builtin_amdgcn_sched_barrier(0);
-	sld(y, S, 2 * l + 1);
-#pragma unroll
-	for (int i = 0; i < 32; i++) x[i] ^= y[i];  // hi = z1 + alpha(z2)
-	sst(S, 2 * l + 1, x);
-	wsync();
-	// lane q's GF(2^64) product P_q = (lo, hi) sits in rows 2q, 2q+1. Lane l assembles limb l:
-	// limbs 0,1 = P00 + P11; limbs 2,3 = P01 + P10 + alpha64(P11), alpha64(P) = (P.hi, P.lo + alpha(P.hi))
-	const int e0 = 2 * (l < 2 ? 0 : 2) + (l & 1);
-	const uint32_t m2 = (l == 2) ? ~0u : 0u, m3 = (l == 3) ? ~0u : 0u;
-	sld(z, S, e0);
-	sld(x, S, e0 + 2);
-#pragma unroll
-	for (int i = 0; i < 32; i++) z[i] ^= x[i];
-	sld(x, S, 3);  // P11.hi
-	bs_alpha<5>(x, y);
-	sld(sa, S, 2);  // P11.lo
-#pragma unroll
-	for (int i = 0; i < 32; i++) z[i] ^= (x[i] & m2) ^ ((sa[i] ^ y[i]) & m3);
-	wsync();
-	sst(S, l, z);
-	wsync();
-}
+using namespace quad;
 
 // out = k * x for a tower constant k < 16 acting on the 8 GF(2^4) coordinates of a limb; c[a]
 // is the GF(2^4) product k * 2^a (host-computed, ScArgs::kcol). Alias-safe.
@@ -344,13 +223,14 @@ struct bn_sumcheck {
 	// which is this prover's sum for round i + 1 (p_i(r) = sum_x prod_j f_j'(x), per shard too).
 	// Round i + 1 then skips point 1 (p(1) = claim + p(0)): (d - 1) fewer products per pair.
 	bool have_pts = false, have_claim = false;
-	uint32_t last_pts[4 * (bn::kMaxD + 1)];
+	uint32_t last_pts[4 * (bn::quad::kMaxD + 1)];
 	uint32_t claim[4];
 };
 
 namespace {
 
 using namespace bn;
+using namespace bn::quad;
 
 int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 	ScArgs A{};

@@ -109,10 +109,12 @@ int bn_gf128_mul_bitsliced_device(const void* d_a, const void* d_b, void* d_out,
 int bn_gf32_mul_device(const void* d_a, const void* d_b, void* d_out, size_t n, void* stream);
 /* Register-resident repeat-loop microbenchmarks in the style of bitsliced_repeat
  * (src/ulvt/finite_fields/tests/profiling/kernels/bitsliced_repeat.cu:5-32):
- * kind 0 = compact GF(2^128), kind 1 = bitsliced GF(2^128) (32 products per lane-block).
- * Each of `threads` lanes performs `iters` dependent products; d_state holds
- * threads*4 (kind 0) or threads*128 (kind 1) words, updated in place, and d_operand holds
- * the lanes' multipliers in the same shape (threads*4 or threads*128 words). */
+ * kind 0 = compact GF(2^128), kind 1 = bitsliced GF(2^128) (32 products per lane-block,
+ * multiply_unrolled<7> per lane), kind 2 = bitsliced GF(2^128) on the quad-lane product of the
+ * sumcheck (one 32-product block per quad of lanes).
+ * Each of `threads` lanes (kinds 0, 1) or blocks (kind 2) performs `iters` dependent products;
+ * d_state holds threads*4 (kind 0) or threads*128 (kinds 1, 2) words, updated in place, and
+ * d_operand holds the multipliers in the same shape. */
 int bn_gf128_mul_repeat_device(int kind, void* d_state, const void* d_operand, size_t threads, int iters, void* stream);
 
 /* ------------------------------------------------------------------------------------

@@ -88,16 +88,16 @@ def test_bitsliced_gf128_mul_kat_and_random(field_kats, dev):
     assert np.array_equal(O.unbitslice128(_np(ta))[:16], np.array(blk["out"], dtype=np.uint32))
 
 
-@pytest.mark.parametrize("kind", [0, 1])
-def test_repeat_microbench_kernels_match_oracle(kind, dev):
-    threads, iters = 64, 3
+@pytest.mark.parametrize("kind,threads", [(0, 64), (1, 64), (2, 64), (2, 70)])
+def test_repeat_microbench_kernels_match_oracle(kind, threads, dev):
+    iters = 3
     words = 4 if kind == 0 else 128
     s0 = _rand(threads * words, 31 + kind)
     op = _rand(threads * words, 41 + kind)
     ts, top = _t(s0, dev), _t(op, dev)
     B.gf128_mul_repeat(kind, ts, top, threads, iters)
     got = _np(ts)
-    if kind == 1:
+    if kind >= 1:
         got, s_c, o_c = O.unbitslice128(got), O.unbitslice128(s0), O.unbitslice128(op)
     else:
         s_c, o_c = s0, op

@@ -51,9 +51,10 @@ def c2(dev, out):
     import binius_ntt_amd as B
     st = torch.cuda.current_stream(dev)
     g = np.random.default_rng(2)
-    for kind, name, words, per in ((0, "compact", 4, 1), (1, "bitsliced", 128, 32)):
+    for kind, name, words, per in ((0, "compact", 4, 1), (1, "bitsliced, multiply_unrolled<7> per lane", 128, 32),
+                                   (2, "bitsliced, quad-lane product", 128, 32)):
         threads = 256 * 2048 if kind == 0 else 256 * 1024
-        iters = 2000 if kind == 0 else 20
+        iters = 2000 if kind == 0 else 20 if kind == 1 else 200
         state = torch.from_numpy(g.integers(0, 2**32, size=threads * words, dtype=np.uint64).astype(np.uint32)
                                  .view(np.int32)).to(dev)
         opnd = torch.from_numpy(g.integers(0, 2**32, size=threads * words, dtype=np.uint64).astype(np.uint32)
