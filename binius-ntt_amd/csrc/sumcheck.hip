@@ -23,8 +23,10 @@
 // folds its 32 result words into one word of parities (bit i = XOR over the elements of bit i),
 // which is exactly the limb of the element-sum that the reference's compute_sum produces.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <vector>
 
 #include "bitsliced.hpp"
@@ -37,7 +39,21 @@ namespace {
 
 constexpr int kScThreads = 256;
 constexpr int kQuadsPerWG = kScThreads / 4;
+// Round messages are XOR-accumulated into kAccCopies copies of the (kMaxD + 1) x 4-word point
+// set, workgroup b into copy b % kAccCopies, each copy on its own 256-B lines: device-scope
+// atomics on one line serialise across the whole grid (about 0.4 ms per c4 run with a single
+// copy), spread over 64 lines they overlap. The host XORs the copies.
+constexpr int kAccCopies = 64;
+constexpr int kAccStride = 64;  // words per copy (>= 4 * (kMaxD + 1))
+constexpr int kAccSet = kAccCopies * kAccStride;
+// Word kAccStride - 1 of copy 0 counts the finished workgroups; the last one XORs the copies and
+// posts the points straight to host-mapped memory, then the round's sequence number in word
+// kResSeq (so the host polls one word instead of queueing a copy and synchronising the stream).
+constexpr int kAccCount = kAccStride - 1;
+constexpr size_t kPostInKernelMaxWG = 64;  // grids up to this post in-kernel (else sc_post)
 using namespace quad;
+static_assert(kAccStride > 4 * (kMaxD + 1), "accumulator copy too small");
+constexpr int kResSeq = 4 * (kMaxD + 1);
 
 // out = k * x for a tower constant k < 16 acting on the 8 GF(2^4) coordinates of a limb; c[a]
 // is the GF(2^4) product k * 2^a (host-computed, ScArgs::kcol). Alias-safe.
@@ -75,15 +91,32 @@ struct ScArgs {
 	int kmax;           // points 0..kmax
 	int skip1;          // point 1 is not computed (the host derives it from the round claim)
 	uint32_t r[4];      // fold challenge
-	uint32_t* acc;      // (kmax + 1) x 4 words, XOR-accumulated (this round's set)
+	uint32_t* acc;      // kAccCopies x (kmax + 1) x 4 words, XOR-accumulated (this round's set)
 	uint32_t* clr;      // the other accumulator set: cleared here for the next round
+	uint32_t* res;      // host-mapped: 4 (kMaxD + 1) point words, then the sequence word
+	uint32_t seq;       // this launch's sequence number
+	int post;           // 1: the last workgroup posts the points (small grids), 0: sc_post does
 	uint32_t kcol[kMaxD + 1][4];  // GF(2^4) products k * 2^a (interpolation point k)
+	int dbg;  // development build (BN_DEV) only: BN_SC_DBG bit 0 = synthetic operands instead of
+	          // column loads, bit 1 = no products, bit 2 = no k-multiples, bit 3 = no parity
+	          // reduction (wrong results; for timing experiments)
 };
 
 // lo/hi limbs of column j for pair p (this lane's limb l)
 template <int MODE>
 __device__ __forceinline__ void load_pair(const ScArgs& A, int j, size_t p, int l, uint32_t* lo, uint32_t* hi, uint32_t& emask) {
 	const uint32_t* c = A.cols + (size_t)j * A.col_stride;
+#ifdef BN_DEV
+	if (A.dbg & 1) {
+#pragma unroll
+		for (int i = 0; i < 32; i++) {
+			lo[i] = (uint32_t)p * 0x9E3779B9u + (uint32_t)(i * 7 + l + j);
+			hi[i] = lo[i] * 0x85EBCA6Bu;
+		}
+		emask = ~0u;
+		return;
+	}
+#endif
 	if constexpr (MODE == 0) {
 		ld32(lo, c + 128 * p + 32 * l);
 		ld32(hi, c + 128 * (p + A.hb) + 32 * l);
@@ -109,6 +142,19 @@ __device__ __forceinline__ void load_pair(const ScArgs& A, int j, size_t p, int 
 	}
 }
 
+// Reduce the accumulator copies and post the points + sequence word to host-mapped memory.
+__device__ __forceinline__ void post_points(const ScArgs& A, int t) {
+	if (t < 4 * (A.kmax + 1)) {
+		uint32_t v = 0;
+		for (int c = 0; c < kAccCopies; c++)
+			v ^= __hip_atomic_load(A.acc + c * kAccStride + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		A.res[t] = v;
+	}
+	__threadfence_system();
+	__syncthreads();
+	if (t == 0) __hip_atomic_store(A.res + kResSeq, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // One (pair, point k) per quad, k fastest: the kmax+1 quads of a pair run side by side, so the
 // pair's columns are read from HBM once and hit in cache for the other points.
 template <int MODE>
@@ -120,7 +166,8 @@ __global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
 	if (threadIdx.x < 4 * (kMaxD + 1)) accL[threadIdx.x] = 0;
 	// rounds alternate between two accumulator sets; the other set was last read back by the
 	// previous round's copy (ordered before this launch), so no memset is queued per round
-	if (blockIdx.x == 0 && threadIdx.x < 4 * (kMaxD + 1)) A.clr[threadIdx.x] = 0;
+	if (blockIdx.x == 0)
+		for (int i = threadIdx.x; i < kAccSet; i += kScThreads) A.clr[i] = 0;
 	__syncthreads();
 	const int npts = A.kmax + 1 - A.skip1;
 	const size_t item = (size_t)blockIdx.x * kQuadsPerWG + qw;
@@ -140,22 +187,56 @@ __global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
 			} else {
 #pragma unroll
 				for (int i = 0; i < 32; i++) hi[i] ^= lo[i];
+#ifdef BN_DEV
+				if (!(A.dbg & 4))
+#endif
 				mul_small(A.kcol[k], hi, hi);
 #pragma unroll
 				for (int i = 0; i < 32; i++) lo[i] ^= hi[i];
 			}
 			sst(S, (j == 0 ? 0 : 4) + l, lo);
+#ifdef BN_DEV
+			if (A.dbg & 2) continue;
+#endif
 			if (j > 0) quad_mul<false>(S, nullptr, l);
 		}
 		wsync();
 		uint32_t t[32];
 		sld(t, S, l);
+#ifdef BN_DEV
+		const uint32_t acc = (A.dbg & 8) ? t[0] ^ t[31] : parity_word(t, emask);
+#else
 		const uint32_t acc = parity_word(t, emask);
+#endif
 		if (acc) atomicXor(accL + 4 * k + l, acc);  // LDS atomic
 	}
 	__syncthreads();
-	if (threadIdx.x < 4 * (A.kmax + 1) && accL[threadIdx.x]) atomicXor(A.acc + threadIdx.x, accL[threadIdx.x]);
+	if (!A.post) {
+		if (threadIdx.x < 4 * (A.kmax + 1) && accL[threadIdx.x])
+			atomicXor(A.acc + (blockIdx.x % kAccCopies) * kAccStride + threadIdx.x, accL[threadIdx.x]);
+		return;  // sc_post follows
+	}
+	// small grids: the last workgroup to finish reduces the copies and posts the points itself
+	if (threadIdx.x < 4 * (A.kmax + 1) && accL[threadIdx.x]) {
+		// a returning atomic: its value is back only once the XOR has been performed, which
+		// orders it before this workgroup's count below without a release fence
+		const uint32_t old = __hip_atomic_fetch_xor(A.acc + (blockIdx.x % kAccCopies) * kAccStride + threadIdx.x,
+													accL[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		asm volatile("" ::"v"(old));
+	}
+	uint32_t* last = accL + 4 * (kMaxD + 1);  // (a static __shared__ word cost a workgroup per CU)
+	__syncthreads();
+	if (threadIdx.x == 0)
+		*last = __hip_atomic_fetch_add(A.acc + kAccCount, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+	__syncthreads();
+	if (!*last) return;
+	__threadfence();
+	post_points(A, threadIdx.x);
 }
+
+// Big grids: a one-wave kernel after sc_messages reduces the copies and posts the points (one
+// counter shared by thousands of workgroups serialised them: 2x the kernel time).
+__global__ __launch_bounds__(64) void sc_post(ScArgs A) { post_points(A, threadIdx.x); }
 
 template <int MODE>
 __global__ __launch_bounds__(kScThreads, 2) void sc_fold(ScArgs A) {
@@ -176,6 +257,9 @@ __global__ __launch_bounds__(kScThreads, 2) void sc_fold(ScArgs A) {
 #pragma unroll
 		for (int i = 0; i < 32; i++) hi[i] ^= lo[i];
 		sst(S, l, hi);
+#ifdef BN_DEV
+		if (!(A.dbg & 2))
+#endif
 		quad_mul<true>(S, R, l);
 		// lo is re-read (cache-resident) rather than kept live across the product
 		load_pair<MODE>(A, j, p, l, lo, hi, emask);
@@ -187,8 +271,49 @@ __global__ __launch_bounds__(kScThreads, 2) void sc_fold(ScArgs A) {
 	}
 }
 
-// quad slots + the fold's broadcast challenge (128 words) + the messages' accumulators
-size_t lds_bytes() { return ((size_t)kQuadsPerWG * kQuadWords + 128 + 4 * (kMaxD + 1)) * sizeof(uint32_t); }
+// Big-mode fold with wave-coalesced global traffic (n_pairs % 16 == 0): a wave's 16 quads take
+// 16 consecutive pairs of one column, so its lo and hi batches are two contiguous 8 KiB runs.
+// Lane t moves 16 B at byte 16 t + 1 KiB i (i < 8) and the LDS slots do the transposition to
+// the quads' limb rows (sc_fold<0>, one 128-B line per lane per instruction, took 13% longer:
+// c4 d=3 round 0, 434 -> 384 us).
+__device__ __forceinline__ uint32_t* coal_addr(uint32_t* wslots, int lane, int i) {
+	const int w = 4 * lane + 256 * i;  // word offset in the wave's 16-batch run
+	return wslots + (w >> 7) * kQuadWords + kRowWords * ((w >> 5) & 3) + (w & 31);
+}
+
+__global__ __launch_bounds__(kScThreads, 2) void sc_fold_coal(ScArgs A) {
+	extern __shared__ uint32_t lds[];
+	const int l = threadIdx.x & 3, qw = threadIdx.x >> 2, lane = threadIdx.x & 63;
+	const Slot S{lds + qw * kQuadWords};
+	uint32_t* wslots = lds + (qw & ~15) * kQuadWords;
+	uint32_t* R = lds + kQuadsPerWG * kQuadWords;
+	if (threadIdx.x < 128) R[threadIdx.x] = 0u - ((A.r[threadIdx.x / 32] >> (threadIdx.x % 32)) & 1u);
+	__syncthreads();
+	const size_t it0 = (size_t)blockIdx.x * kQuadsPerWG + (qw & ~15);  // the wave's first item
+	if (it0 >= (size_t)A.d * A.n_pairs) return;
+	const int j = (int)(it0 / A.n_pairs);
+	const size_t p0 = it0 % A.n_pairs;
+	uint32_t* lo = A.cols + (size_t)j * A.col_stride + 128 * p0;
+	const uint32_t* hi = lo + 128 * A.hb;
+#pragma unroll
+	for (int i = 0; i < 8; i++) {
+		const uint4 a = *(const uint4*)(lo + 4 * lane + 256 * i), b = *(const uint4*)(hi + 4 * lane + 256 * i);
+		*(uint4*)coal_addr(wslots, lane, i) = make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
+	}
+#ifdef BN_DEV
+	if (!(A.dbg & 2))
+#endif
+	quad_mul<true>(S, R, l);
+	wsync();
+#pragma unroll
+	for (int i = 0; i < 8; i++) {
+		const uint4 a = *(const uint4*)(lo + 4 * lane + 256 * i), q = *(const uint4*)coal_addr(wslots, lane, i);
+		*(uint4*)(lo + 4 * lane + 256 * i) = make_uint4(a.x ^ q.x, a.y ^ q.y, a.z ^ q.z, a.w ^ q.w);
+	}
+}
+
+// quad slots + the fold's broadcast challenge (128 words) + the messages' accumulators and flag
+size_t lds_bytes() { return ((size_t)kQuadsPerWG * kQuadWords + 128 + 4 * (kMaxD + 1) + 1) * sizeof(uint32_t); }
 
 struct DeviceScope {
 	int prev = -1;
@@ -214,17 +339,20 @@ struct bn_sumcheck {
 	size_t cur = 0;         // evaluations per column held by this prover
 	size_t col_words = 0;   // words between columns (allocation)
 	uint32_t* cols = nullptr;
-	uint32_t* acc = nullptr;    // 2 sets of 4 * (kMaxD + 1) words, alternating rounds
+	uint32_t* acc = nullptr;    // 2 sets of kAccSet words (see kAccCopies), alternating rounds
 	int par = 0;                // set used by the next round_messages
-	uint32_t* h_acc = nullptr;  // pinned host copy of acc (round messages)
+	uint32_t* h_res = nullptr;  // host-mapped, GPU-coherent: the round's points + sequence word
+	uint32_t* d_res = nullptr;  // its device address
+	uint32_t seq = 0;
 	hipStream_t stream = nullptr;
 	bool sharded_used = false;
 	// Round claim: once round i's points are known, move_to_next_round(r) interpolates them at r,
 	// which is this prover's sum for round i + 1 (p_i(r) = sum_x prod_j f_j'(x), per shard too).
 	// Round i + 1 then skips point 1 (p(1) = claim + p(0)): (d - 1) fewer products per pair.
-	bool have_pts = false, have_claim = false;
+	// The interpolation itself runs in the next round_messages, while its kernel is in flight.
+	bool have_pts = false, have_claim = false, claim_pending = false;
 	uint32_t last_pts[4 * (bn::quad::kMaxD + 1)];
-	uint32_t claim[4];
+	uint32_t claim[4], pending_r[4];
 };
 
 namespace {
@@ -252,20 +380,31 @@ int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 		A.n_pairs = 1;
 		A.kmax = 0;
 	}
-	A.skip1 = (!fold && sc->have_claim && A.mode != 2) ? 1 : 0;
-	A.acc = sc->acc + 4 * (kMaxD + 1) * sc->par;
-	A.clr = sc->acc + 4 * (kMaxD + 1) * (1 - sc->par);
+	A.skip1 = (!fold && (sc->have_claim || sc->claim_pending) && A.mode != 2) ? 1 : 0;
+	A.res = sc->d_res;
+	if (!fold) A.seq = ++sc->seq;
+	A.acc = sc->acc + kAccSet * sc->par;
+	A.clr = sc->acc + kAccSet * (1 - sc->par);
 	if (fold) memcpy(A.r, r, 16);
+#ifdef BN_DEV
+	{
+		static const int dbg = getenv("BN_SC_DBG") ? atoi(getenv("BN_SC_DBG")) : 0;
+		A.dbg = dbg;
+	}
+#endif
 	for (int k = 0; k <= kMaxD; k++)
 		for (int a = 0; a < 4; a++) A.kcol[k][a] = (uint32_t)tw_mul((uint64_t)k, 1ull << a, 2);
 	// one item per quad: fold (column, pair), messages (pair, point)
 	const size_t items = fold ? (size_t)sc->d * A.n_pairs : A.n_pairs * (size_t)(A.kmax + 1 - A.skip1);
 	const size_t grid = (items + kQuadsPerWG - 1) / kQuadsPerWG;
 	void* args[] = {&A};
+	const bool coal = fold && A.mode == 0 && A.n_pairs % 16 == 0;
 	const void* fns[2][3] = {{(const void*)sc_messages<0>, (const void*)sc_messages<1>, (const void*)sc_messages<2>},
-							 {(const void*)sc_fold<0>, (const void*)sc_fold<1>, (const void*)sc_fold<2>}};
+							 {coal ? (const void*)sc_fold_coal : (const void*)sc_fold<0>, (const void*)sc_fold<1>, (const void*)sc_fold<2>}};
+	A.post = grid <= kPostInKernelMaxWG;
 	BN_HIP(hipLaunchKernel(fns[fold ? 1 : 0][A.mode], dim3((unsigned)grid), dim3(kScThreads),
 						   args, lds_bytes(), sc->stream));
+	if (!fold && !A.post) BN_HIP(hipLaunchKernel((const void*)sc_post, dim3(1), dim3(64), args, 0, sc->stream));
 	return BN_OK;
 }
 
@@ -277,11 +416,14 @@ int sc_alloc(bn_sumcheck* sc, size_t col_words) {
 
 int sc_common_init(bn_sumcheck* sc) {
 	BN_HIP(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
-	BN_HIP(hipMalloc(&sc->acc, sizeof(uint32_t) * 8 * (kMaxD + 1)));
-	BN_HIP(hipMemsetAsync(sc->acc, 0, sizeof(uint32_t) * 8 * (kMaxD + 1), sc->stream));
-	BN_HIP(hipHostMalloc((void**)&sc->h_acc, sizeof(uint32_t) * 4 * (kMaxD + 1), hipHostMallocDefault));
-	const void* fns[6] = {(const void*)sc_messages<0>, (const void*)sc_messages<1>, (const void*)sc_messages<2>,
-						  (const void*)sc_fold<0>,     (const void*)sc_fold<1>,     (const void*)sc_fold<2>};
+	BN_HIP(hipMalloc(&sc->acc, sizeof(uint32_t) * 2 * kAccSet));
+	BN_HIP(hipMemsetAsync(sc->acc, 0, sizeof(uint32_t) * 2 * kAccSet, sc->stream));
+	BN_HIP(hipHostMalloc((void**)&sc->h_res, sizeof(uint32_t) * (kResSeq + 1), hipHostMallocMapped | hipHostMallocCoherent));
+	memset(sc->h_res, 0, sizeof(uint32_t) * (kResSeq + 1));
+	BN_HIP(hipHostGetDevicePointer((void**)&sc->d_res, sc->h_res, 0));
+	const void* fns[7] = {(const void*)sc_messages<0>, (const void*)sc_messages<1>, (const void*)sc_messages<2>,
+						  (const void*)sc_fold<0>,     (const void*)sc_fold<1>,     (const void*)sc_fold<2>,
+						  (const void*)sc_fold_coal};
 	for (const void* f : fns) BN_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes()));
 	return BN_OK;
 }
@@ -291,7 +433,7 @@ void sc_free(bn_sumcheck* sc) {
 	if (sc->stream) (void)hipStreamSynchronize(sc->stream);
 	if (sc->cols) (void)hipFree(sc->cols);
 	if (sc->acc) (void)hipFree(sc->acc);
-	if (sc->h_acc) (void)hipHostFree(sc->h_acc);
+	if (sc->h_res) (void)hipHostFree(sc->h_res);
 	if (sc->stream) (void)hipStreamDestroy(sc->stream);
 	delete sc;
 }
@@ -536,7 +678,7 @@ extern "C" int bn_sumcheck_import_gathered(bn_sumcheck* sc, const uint32_t* word
 	sc->cur = (size_t)32 * world;
 	sc->rank = 0;
 	sc->world = 1;
-	sc->have_pts = sc->have_claim = false;  // the shards' claims are partial: recompute point 1
+	sc->have_pts = sc->have_claim = sc->claim_pending = false;  // the shards' claims are partial: recompute point 1
 	return BN_OK;
 }
 
@@ -546,12 +688,32 @@ extern "C" int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32
 	DeviceScope ds(sc->device);
 	int rc = sc_launch(sc, false, nullptr);
 	if (rc != BN_OK) return rc;
-	const uint32_t* acc = sc->h_acc;
-	BN_HIP(hipMemcpyAsync(sc->h_acc, sc->acc + 4 * (kMaxD + 1) * sc->par, sizeof(uint32_t) * 4 * (kMaxD + 1),
-						  hipMemcpyDeviceToHost, sc->stream));
 	sc->par ^= 1;
-	BN_HIP(hipStreamSynchronize(sc->stream));
+	if (sc->claim_pending) {  // last round's claim, computed while this round's kernel runs
+		rc = bn_sumcheck_interpolate(sc->last_pts, sc->d + 1, sc->pending_r, sc->claim);
+		if (rc != BN_OK) return rc;
+		sc->claim_pending = false;
+		sc->have_claim = sc->cur > 1;
+	}
+	// wait for the posted sequence number (the stream is queried between polls, so a failed
+	// kernel is reported rather than waited for)
+	const volatile uint32_t* posted = sc->h_res + kResSeq;
+	for (;;) {
+		bool seen = false;
+		for (int i = 0; i < 4096 && !(seen = *posted == sc->seq); i++) {
+		}
+		if (seen) break;
+		const hipError_t e = hipStreamQuery(sc->stream);
+		if (e == hipSuccess) {
+			if (*posted == sc->seq) break;
+			BN_FAIL(BN_ERR_HIP, "round messages were not posted (sequence %u)", sc->seq);
+		}
+		if (e != hipErrorNotReady) BN_FAIL(BN_ERR_HIP, "round messages kernel: %s", hipGetErrorString(e));
+	}
+	std::atomic_thread_fence(std::memory_order_acquire);
 	const int npts = sc->d + 1;
+	uint32_t acc[4 * (kMaxD + 1)];
+	for (int i = 0; i < 4 * npts; i++) acc[i] = ((const volatile uint32_t*)sc->h_res)[i];
 	if (sc->cur == 1) {
 		memcpy(sum, acc, 16);  // mode 2 computed prod_j f_j(0) as "point 0"
 		memset(points, 0, sizeof(uint32_t) * 4 * npts);
@@ -582,12 +744,9 @@ extern "C" int bn_sumcheck_move_to_next_round(bn_sumcheck* sc, const uint32_t* c
 	if (rc != BN_OK) return rc;
 	// no sync: the fold is ordered before the next round's messages on the prover's stream
 	sc->have_claim = false;  // a claim not consumed by this round's messages is stale now
-	if (sc->have_pts) {
-		rc = bn_sumcheck_interpolate(sc->last_pts, sc->d + 1, challenge, sc->claim);
-		if (rc != BN_OK) return rc;
-		sc->have_claim = true;
-		sc->have_pts = false;
-	}
+	sc->claim_pending = sc->have_pts;
+	if (sc->have_pts) memcpy(sc->pending_r, challenge, 16);
+	sc->have_pts = false;
 	sc->cur /= 2;
 	sc->round++;
 	sc->sharded_used = true;
