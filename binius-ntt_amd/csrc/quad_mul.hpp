@@ -135,5 +135,77 @@ __device__ __forceinline__ void quad_mul(const Slot& S, const uint32_t* B, int l
 	wsync();
 }
 
+// Low-latency GF(2^128) product on a group of 16 lanes, for launches too small to fill the GPU
+// (the sumcheck's last rounds): the 12 GF(2^32) products of the schoolbook-over-Karatsuba split
+// run side by side, one per lane, instead of 3 in sequence per lane of a quad.
+//   lane s < 12: q = s / 3 (P_q = A_i B_j as in quad_mul), t = s % 3 (Karatsuba z0, z2, z1)
+//   lane s < 8 : P_{s/2} half s%2 (lo = z0 + z2, hi = z1 + z0 + z2 + alpha(z2))
+//   lane s < 4 : limb s of the product
+// Slot rows: 0-3 operand A, 4-7 operand B (then the P halves), 8-19 the z's, 20-23 alpha(z2).
+constexpr int kHexWords = 24 * kRowWords + 16;
+
+template <bool B_SHARED>
+__device__ __forceinline__ void hex_mul(const Slot& S, const uint32_t* B, int s) {
+	wsync();
+	if (s < 12) {
+		const int q = s / 3, t = s - 3 * (s / 3);
+		const int ia = q & 1, jb = (q == 1 || q == 2) ? 1 : 0;
+		const int ra = 2 * ia + (t == 1), rb = 2 * jb + (t == 1);  // z0: (lo, lo), z2: (hi, hi)
+		const uint32_t m = t == 2 ? ~0u : 0u;                     // z1: (lo + hi, lo + hi)
+		const uint32_t* A0 = S.row(ra);
+		const uint32_t* A1 = S.row(2 * ia + 1);
+		const uint32_t* B0 = B_SHARED ? B + 32 * rb : S.row(4 + rb);
+		const uint32_t* B1 = B_SHARED ? B + 64 * jb + 32 : S.row(4 + 2 * jb + 1);
+		uint32_t x[32], y[32], z[32];
+#pragma unroll
+		for (int i = 0; i < 32; i += 4) {
+			const uint4 p = *(const uint4*)(A0 + i), p1 = *(const uint4*)(A1 + i);
+			const uint4 u = *(const uint4*)(B0 + i), u1 = *(const uint4*)(B1 + i);
+			x[i] = p.x ^ (p1.x & m), x[i + 1] = p.y ^ (p1.y & m), x[i + 2] = p.z ^ (p1.z & m), x[i + 3] = p.w ^ (p1.w & m);
+			y[i] = u.x ^ (u1.x & m), y[i + 1] = u.y ^ (u1.y & m), y[i + 2] = u.z ^ (u1.z & m), y[i + 3] = u.w ^ (u1.w & m);
+		}
+		__builtin_amdgcn_sched_barrier(0);
+		bsm5_mul(x, y, z);
+		__builtin_amdgcn_sched_barrier(0);
+		sst(S, 8 + s, z);
+		if (t == 1) {
+			bs_alpha<5>(z, x);
+			sst(S, 20 + q, x);
+		}
+	}
+	wsync();
+	if (s < 8) {  // P_q.lo = z0 + z2, P_q.hi = P_q.lo + z1 + alpha(z2)
+		const int q = s >> 1;
+		const uint32_t m = (s & 1) ? ~0u : 0u;
+		const uint32_t *z0 = S.row(8 + 3 * q), *z2 = S.row(9 + 3 * q), *z1 = S.row(10 + 3 * q), *az = S.row(20 + q);
+		uint32_t r[32];
+#pragma unroll
+		for (int i = 0; i < 32; i++) r[i] = z0[i] ^ z2[i] ^ ((z1[i] ^ az[i]) & m);
+		wsync();  // the operand rows are free once every lane has passed the first phase
+		sst(S, 4 + s, r);
+	}
+	wsync();
+	if (s < 4) {
+		// limb 0 = P0.lo + P1.lo, 1 = P0.hi + P1.hi, 2 = P2.lo + P3.lo + P1.hi,
+		// limb 3 = P2.hi + P3.hi + P1.lo + alpha(P1.hi)   (P_q half h in row 4 + 2q + h)
+		const int h = s & 1, qa = s < 2 ? 0 : 2;
+		const uint32_t m2 = s >= 2 ? ~0u : 0u;
+		const uint32_t *pa = S.row(4 + 2 * qa + h), *pb = S.row(6 + 2 * qa + h), *pc = S.row(s == 2 ? 7 : 6);
+		uint32_t r[32];
+#pragma unroll
+		for (int i = 0; i < 32; i++) r[i] = pa[i] ^ pb[i] ^ (pc[i] & m2);
+		if (s == 3) {
+			uint32_t x[32], y[32];
+			sld(x, S, 7);
+			bs_alpha<5>(x, y);
+#pragma unroll
+			for (int i = 0; i < 32; i++) r[i] ^= y[i];
+		}
+		wsync();
+		sst(S, s, r);
+	}
+	wsync();
+}
+
 }  // namespace quad
 }  // namespace bn

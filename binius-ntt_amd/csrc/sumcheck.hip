@@ -26,6 +26,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <vector>
 
@@ -51,6 +52,7 @@ constexpr int kAccSet = kAccCopies * kAccStride;
 // kResSeq (so the host polls one word instead of queueing a copy and synchronising the stream).
 constexpr int kAccCount = kAccStride - 1;
 constexpr size_t kPostInKernelMaxWG = 64;  // grids up to this post in-kernel (else sc_post)
+constexpr size_t kHexMaxItems = 8192;      // launches up to this many items use 16-lane products
 using namespace quad;
 static_assert(kAccStride > 4 * (kMaxD + 1), "accumulator copy too small");
 constexpr int kResSeq = 4 * (kMaxD + 1);
@@ -155,14 +157,31 @@ __device__ __forceinline__ void post_points(const ScArgs& A, int t) {
 	if (t == 0) __hip_atomic_store(A.res + kResSeq, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// One (pair, point k) per quad, k fastest: the kmax+1 quads of a pair run side by side, so the
+// Products run on a group of G lanes: G = 4 (quad_mul, throughput) for launches that fill the
+// GPU, G = 16 (hex_mul, about a third of the latency) for the last rounds' small launches. Lanes
+// l < 4 of a group hold the limbs of the operands and results.
+template <int G>
+struct Grp {
+	static constexpr int kGroups = kScThreads / G;
+	static constexpr int kSlotWords = G == 4 ? kQuadWords : kHexWords;
+	static constexpr int kSlotsWords = kGroups * kSlotWords;
+};
+template <int G, bool B_SHARED>
+__device__ __forceinline__ void grp_mul(const Slot& S, const uint32_t* B, int l) {
+	if constexpr (G == 4)
+		quad_mul<B_SHARED>(S, B, l);
+	else
+		hex_mul<B_SHARED>(S, B, l);
+}
+
+// One (pair, point k) per group, k fastest: the kmax+1 groups of a pair run side by side, so the
 // pair's columns are read from HBM once and hit in cache for the other points.
-template <int MODE>
+template <int MODE, int G>
 __global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
 	extern __shared__ uint32_t lds[];
-	const int l = threadIdx.x & 3, qw = threadIdx.x >> 2;
-	const Slot S{lds + qw * kQuadWords};
-	uint32_t* accL = lds + kQuadsPerWG * kQuadWords + 128;  // (kMaxD + 1) x 4 words
+	const int l = threadIdx.x % G, qw = threadIdx.x / G;
+	const Slot S{lds + qw * Grp<G>::kSlotWords};
+	uint32_t* accL = lds + Grp<G>::kSlotsWords + 128;  // (kMaxD + 1) x 4 words
 	if (threadIdx.x < 4 * (kMaxD + 1)) accL[threadIdx.x] = 0;
 	// rounds alternate between two accumulator sets; the other set was last read back by the
 	// previous round's copy (ordered before this launch), so no memset is queued per round
@@ -170,7 +189,7 @@ __global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
 		for (int i = threadIdx.x; i < kAccSet; i += kScThreads) A.clr[i] = 0;
 	__syncthreads();
 	const int npts = A.kmax + 1 - A.skip1;
-	const size_t item = (size_t)blockIdx.x * kQuadsPerWG + qw;
+	const size_t item = (size_t)blockIdx.x * Grp<G>::kGroups + qw;
 	const size_t p = item / npts;
 	const int ki = (int)(item % npts);
 	const int k = (A.skip1 && ki >= 1) ? ki + 1 : ki;
@@ -178,6 +197,7 @@ __global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
 		uint32_t emask = 0;
 		for (int j = 0; j < A.d; j++) {
 			// f_j at point k: lo + k (lo + hi), written into the A (j == 0) or B operand
+			if (l < 4) {
 			uint32_t lo[32], hi[32];
 			load_pair<MODE>(A, j, p, l, lo, hi, emask);
 			if (k == 0) {
@@ -195,12 +215,14 @@ __global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
 				for (int i = 0; i < 32; i++) lo[i] ^= hi[i];
 			}
 			sst(S, (j == 0 ? 0 : 4) + l, lo);
+			}
 #ifdef BN_DEV
 			if (A.dbg & 2) continue;
 #endif
-			if (j > 0) quad_mul<false>(S, nullptr, l);
+			if (j > 0) grp_mul<G, false>(S, nullptr, l);
 		}
 		wsync();
+		if (l < 4) {
 		uint32_t t[32];
 		sld(t, S, l);
 #ifdef BN_DEV
@@ -209,6 +231,7 @@ __global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
 		const uint32_t acc = parity_word(t, emask);
 #endif
 		if (acc) atomicXor(accL + 4 * k + l, acc);  // LDS atomic
+		}
 	}
 	__syncthreads();
 	if (!A.post) {
@@ -238,29 +261,31 @@ __global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
 // counter shared by thousands of workgroups serialised them: 2x the kernel time).
 __global__ __launch_bounds__(64) void sc_post(ScArgs A) { post_points(A, threadIdx.x); }
 
-template <int MODE>
+template <int MODE, int G>
 __global__ __launch_bounds__(kScThreads, 2) void sc_fold(ScArgs A) {
 	extern __shared__ uint32_t lds[];
-	const int l = threadIdx.x & 3, qw = threadIdx.x >> 2;
-	const Slot S{lds + qw * kQuadWords};
-	uint32_t* R = lds + kQuadsPerWG * kQuadWords;  // the challenge, broadcast-bitsliced, shared
+	const int l = threadIdx.x % G, qw = threadIdx.x / G;
+	const Slot S{lds + qw * Grp<G>::kSlotWords};
+	uint32_t* R = lds + Grp<G>::kSlotsWords;  // the challenge, broadcast-bitsliced, shared
 	if (threadIdx.x < 128) R[threadIdx.x] = 0u - ((A.r[threadIdx.x / 32] >> (threadIdx.x % 32)) & 1u);
 	__syncthreads();
-	const size_t quad0 = (size_t)blockIdx.x * kQuadsPerWG + qw;
 	const size_t items = (size_t)A.d * A.n_pairs;
-	const size_t it = quad0;
-	if (it < items) {  // one item per quad (no grid-stride loop: it costs registers)
+	const size_t it = (size_t)blockIdx.x * Grp<G>::kGroups + qw;
+	if (it < items) {  // one item per group (no grid-stride loop: it costs registers)
 		const int j = (int)(it / A.n_pairs);
 		const size_t p = it % A.n_pairs;
 		uint32_t lo[32], hi[32], emask;
-		load_pair<MODE>(A, j, p, l, lo, hi, emask);
+		if (l < 4) {
+			load_pair<MODE>(A, j, p, l, lo, hi, emask);
 #pragma unroll
-		for (int i = 0; i < 32; i++) hi[i] ^= lo[i];
-		sst(S, l, hi);
+			for (int i = 0; i < 32; i++) hi[i] ^= lo[i];
+			sst(S, l, hi);
+		}
 #ifdef BN_DEV
 		if (!(A.dbg & 2))
 #endif
-		quad_mul<true>(S, R, l);
+		grp_mul<G, true>(S, R, l);
+		if (l >= 4) return;
 		// lo is re-read (cache-resident) rather than kept live across the product
 		load_pair<MODE>(A, j, p, l, lo, hi, emask);
 		sld(hi, S, l);
@@ -313,7 +338,8 @@ __global__ __launch_bounds__(kScThreads, 2) void sc_fold_coal(ScArgs A) {
 }
 
 // quad slots + the fold's broadcast challenge (128 words) + the messages' accumulators and flag
-size_t lds_bytes() { return ((size_t)kQuadsPerWG * kQuadWords + 128 + 4 * (kMaxD + 1) + 1) * sizeof(uint32_t); }
+template <int G>
+size_t lds_bytes() { return ((size_t)Grp<G>::kSlotsWords + 128 + 4 * (kMaxD + 1) + 1) * sizeof(uint32_t); }
 
 struct DeviceScope {
 	int prev = -1;
@@ -353,6 +379,9 @@ struct bn_sumcheck {
 	bool have_pts = false, have_claim = false, claim_pending = false;
 	uint32_t last_pts[4 * (bn::quad::kMaxD + 1)];
 	uint32_t claim[4], pending_r[4];
+	// move_to_next_round queues the next round's messages kernel right behind the fold, so the
+	// GPU never waits for the host's next call (composition_eval, which only folds, does not)
+	bool msgs_queued = false, eager = true;
 };
 
 namespace {
@@ -394,17 +423,30 @@ int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 #endif
 	for (int k = 0; k <= kMaxD; k++)
 		for (int a = 0; a < 4; a++) A.kcol[k][a] = (uint32_t)tw_mul((uint64_t)k, 1ull << a, 2);
-	// one item per quad: fold (column, pair), messages (pair, point)
+	// one item per lane group: fold (column, pair), messages (pair, point)
 	const size_t items = fold ? (size_t)sc->d * A.n_pairs : A.n_pairs * (size_t)(A.kmax + 1 - A.skip1);
-	const size_t grid = (items + kQuadsPerWG - 1) / kQuadsPerWG;
+	const bool hex = items <= kHexMaxItems;
+	const size_t per_wg = hex ? Grp<16>::kGroups : Grp<4>::kGroups;
+	const size_t grid = (items + per_wg - 1) / per_wg;
 	void* args[] = {&A};
-	const bool coal = fold && A.mode == 0 && A.n_pairs % 16 == 0;
-	const void* fns[2][3] = {{(const void*)sc_messages<0>, (const void*)sc_messages<1>, (const void*)sc_messages<2>},
-							 {coal ? (const void*)sc_fold_coal : (const void*)sc_fold<0>, (const void*)sc_fold<1>, (const void*)sc_fold<2>}};
+	const bool coal = fold && !hex && A.mode == 0 && A.n_pairs % 16 == 0;
+	const void* fns[2][2][3] = {
+		{{(const void*)sc_messages<0, 4>, (const void*)sc_messages<1, 4>, (const void*)sc_messages<2, 4>},
+		 {coal ? (const void*)sc_fold_coal : (const void*)sc_fold<0, 4>, (const void*)sc_fold<1, 4>, (const void*)sc_fold<2, 4>}},
+		{{(const void*)sc_messages<0, 16>, (const void*)sc_messages<1, 16>, (const void*)sc_messages<2, 16>},
+		 {(const void*)sc_fold<0, 16>, (const void*)sc_fold<1, 16>, (const void*)sc_fold<2, 16>}}};
 	A.post = grid <= kPostInKernelMaxWG;
-	BN_HIP(hipLaunchKernel(fns[fold ? 1 : 0][A.mode], dim3((unsigned)grid), dim3(kScThreads),
-						   args, lds_bytes(), sc->stream));
+	BN_HIP(hipLaunchKernel(fns[hex][fold ? 1 : 0][A.mode], dim3((unsigned)grid), dim3(kScThreads), args,
+						   hex ? lds_bytes<16>() : lds_bytes<4>(), sc->stream));
 	if (!fold && !A.post) BN_HIP(hipLaunchKernel((const void*)sc_post, dim3(1), dim3(64), args, 0, sc->stream));
+	return BN_OK;
+}
+
+int queue_messages(bn_sumcheck* sc) {
+	int rc = sc_launch(sc, false, nullptr);
+	if (rc != BN_OK) return rc;
+	sc->par ^= 1;
+	sc->msgs_queued = true;
 	return BN_OK;
 }
 
@@ -421,10 +463,13 @@ int sc_common_init(bn_sumcheck* sc) {
 	BN_HIP(hipHostMalloc((void**)&sc->h_res, sizeof(uint32_t) * (kResSeq + 1), hipHostMallocMapped | hipHostMallocCoherent));
 	memset(sc->h_res, 0, sizeof(uint32_t) * (kResSeq + 1));
 	BN_HIP(hipHostGetDevicePointer((void**)&sc->d_res, sc->h_res, 0));
-	const void* fns[7] = {(const void*)sc_messages<0>, (const void*)sc_messages<1>, (const void*)sc_messages<2>,
-						  (const void*)sc_fold<0>,     (const void*)sc_fold<1>,     (const void*)sc_fold<2>,
-						  (const void*)sc_fold_coal};
-	for (const void* f : fns) BN_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes()));
+	const void* fns[13] = {(const void*)sc_messages<0, 4>,  (const void*)sc_messages<1, 4>,  (const void*)sc_messages<2, 4>,
+						   (const void*)sc_fold<0, 4>,      (const void*)sc_fold<1, 4>,      (const void*)sc_fold<2, 4>,
+						   (const void*)sc_messages<0, 16>, (const void*)sc_messages<1, 16>, (const void*)sc_messages<2, 16>,
+						   (const void*)sc_fold<0, 16>,     (const void*)sc_fold<1, 16>,     (const void*)sc_fold<2, 16>,
+						   (const void*)sc_fold_coal};
+	for (const void* f : fns)
+		BN_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max(lds_bytes<4>(), lds_bytes<16>())));
 	return BN_OK;
 }
 
@@ -679,6 +724,7 @@ extern "C" int bn_sumcheck_import_gathered(bn_sumcheck* sc, const uint32_t* word
 	sc->rank = 0;
 	sc->world = 1;
 	sc->have_pts = sc->have_claim = sc->claim_pending = false;  // the shards' claims are partial: recompute point 1
+	sc->msgs_queued = false;
 	return BN_OK;
 }
 
@@ -686,9 +732,12 @@ extern "C" int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32
 	BN_CHECK_ARG(sc && sum && points, "NULL argument");
 	BN_CHECK_ARG(!(sc->world > 1 && sc->cur <= 32), "shard exhausted: gather (export_shard/import_gathered) first");
 	DeviceScope ds(sc->device);
-	int rc = sc_launch(sc, false, nullptr);
-	if (rc != BN_OK) return rc;
-	sc->par ^= 1;
+	if (!sc->msgs_queued) {
+		int rc = queue_messages(sc);
+		if (rc != BN_OK) return rc;
+	}
+	sc->msgs_queued = false;
+	int rc = BN_OK;
 	if (sc->claim_pending) {  // last round's claim, computed while this round's kernel runs
 		rc = bn_sumcheck_interpolate(sc->last_pts, sc->d + 1, sc->pending_r, sc->claim);
 		if (rc != BN_OK) return rc;
@@ -750,6 +799,8 @@ extern "C" int bn_sumcheck_move_to_next_round(bn_sumcheck* sc, const uint32_t* c
 	sc->cur /= 2;
 	sc->round++;
 	sc->sharded_used = true;
+	sc->msgs_queued = false;  // a queued, unread messages kernel ran before the fold: dropped
+	if (sc->eager && !(sc->world > 1 && sc->cur <= 32)) return queue_messages(sc);
 	return BN_OK;
 }
 
@@ -774,6 +825,7 @@ namespace {
 int composition_eval(bn_sumcheck* sc, const uint32_t* challenges, uint32_t* out) {
 	// folding every column at r_0, r_1, ... (highest variable first) leaves f_j(r); the last
 	// round's "sum" is then prod_j f_j(r)
+	sc->eager = false;
 	for (int i = 0; i < sc->num_vars; i++) {
 		int rc = bn_sumcheck_move_to_next_round(sc, challenges + 4 * (size_t)i);
 		if (rc != BN_OK) return rc;

@@ -506,8 +506,19 @@ class Sumcheck:
             _check(lib().bn_sumcheck_create_device(device, num_vars, composition_size,
                                                    1 if data_is_transposed else 0, _ptr(evals), 0, ctypes.byref(p)))
         self._sc = p
+        self._bind()
         if shard is not None:
             _check(lib().bn_sumcheck_set_shard(self._sc, shard[0], shard[1]))
+
+    def _bind(self):
+        # per-round calls are on the protocol's critical path (the GPU waits for the host's
+        # challenge): resolve the entry points and the output buffers' pointers once
+        L, u32p = lib(), ctypes.POINTER(ctypes.c_uint32)
+        self._f_msgs, self._f_next = L.bn_sumcheck_round_messages, L.bn_sumcheck_move_to_next_round
+        self._sum_buf = np.zeros(4, np.uint32)
+        self._pts_buf = np.zeros(4 * (self.d + 1), np.uint32)
+        self._ch_buf = np.zeros(4, np.uint32)
+        self._sum_p, self._pts_p, self._ch_p = (b.ctypes.data_as(u32p) for b in (self._sum_buf, self._pts_buf, self._ch_buf))
 
     @classmethod
     def from_shard(cls, num_vars, composition_size, local_evals, rank, world, device=0, stream=None):
@@ -522,18 +533,20 @@ class Sumcheck:
                                                      _ptr(local_evals), _stream(stream, local_evals.device.index),
                                                      ctypes.byref(p)))
         self._sc = p
+        self._bind()
         return self
 
     def this_round_messages(self):
-        s = np.zeros(4, np.uint32)
-        pts = np.zeros(4 * (self.d + 1), np.uint32)
-        _check(lib().bn_sumcheck_round_messages(self._sc, s.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
-                                                pts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))))
-        return s, pts.reshape(self.d + 1, 4)
+        rc = self._f_msgs(self._sc, self._sum_p, self._pts_p)
+        if rc != BN_OK:
+            _check(rc)
+        return self._sum_buf.copy(), self._pts_buf.reshape(self.d + 1, 4).copy()
 
     def move_to_next_round(self, challenge):
-        c = np.ascontiguousarray(challenge, dtype=np.uint32).reshape(4)
-        _check(lib().bn_sumcheck_move_to_next_round(self._sc, c.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))))
+        self._ch_buf[:] = np.asarray(challenge, dtype=np.uint32).reshape(4)
+        rc = self._f_next(self._sc, self._ch_p)
+        if rc != BN_OK:
+            _check(rc)
 
     def round(self):
         r = ctypes.c_int()
