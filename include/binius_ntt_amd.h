@@ -167,9 +167,11 @@ int bn_sumcheck_create(int device, int num_vars, int composition_size, int data_
 int bn_sumcheck_create_device(int device, int num_vars, int composition_size, int data_is_transposed,
                               void* d_evals, int take_ownership, bn_sumcheck** sc);
 /* Replaces Sumcheck::this_round_messages(sum, points) (sumcheck.cuh:130-246):
- * sum[4], points[4*(composition_size+1)] (round polynomial at 0..d). */
+ * sum[4], points[4*(composition_size+1)] (round polynomial at 0..d). Blocks until the round's
+ * points are posted (the calling thread polls host memory). */
 int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32_t* points);
-/* Replaces Sumcheck::move_to_next_round(challenge) (sumcheck.cuh:248-300). */
+/* Replaces Sumcheck::move_to_next_round(challenge) (sumcheck.cuh:248-300). Asynchronous: queues
+ * the fold and the next round's messages kernel on the prover's stream and returns. */
 int bn_sumcheck_move_to_next_round(bn_sumcheck* sc, const uint32_t* challenge);
 /* Current round (0 .. num_vars). */
 int bn_sumcheck_round(const bn_sumcheck* sc, int* round);
