@@ -38,7 +38,8 @@
 namespace bn {
 namespace {
 
-constexpr int kScThreads = 256;
+constexpr int kScThreads = 256;  // (512-thread workgroups, one per CU: 6 % slower on c4)
+constexpr int kScMinWG = 512 / kScThreads;  // 2 waves per SIMD (256 VGPRs)
 constexpr int kQuadsPerWG = kScThreads / 4;
 // Round messages are XOR-accumulated into kAccCopies copies of the (kMaxD + 1) x 4-word point
 // set, workgroup b into copy b % kAccCopies, each copy on its own 256-B lines: device-scope
@@ -177,7 +178,7 @@ __device__ __forceinline__ void grp_mul(const Slot& S, const uint32_t* B, int l)
 // One (pair, point k) per group, k fastest: the kmax+1 groups of a pair run side by side, so the
 // pair's columns are read from HBM once and hit in cache for the other points.
 template <int MODE, int G>
-__global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
+__global__ __launch_bounds__(kScThreads, kScMinWG) void sc_messages(ScArgs A) {
 	extern __shared__ uint32_t lds[];
 	const int l = threadIdx.x % G, qw = threadIdx.x / G;
 	const Slot S{lds + qw * Grp<G>::kSlotWords};
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(kScThreads, 2) void sc_messages(ScArgs A) {
 __global__ __launch_bounds__(64) void sc_post(ScArgs A) { post_points(A, threadIdx.x); }
 
 template <int MODE, int G>
-__global__ __launch_bounds__(kScThreads, 2) void sc_fold(ScArgs A) {
+__global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold(ScArgs A) {
 	extern __shared__ uint32_t lds[];
 	const int l = threadIdx.x % G, qw = threadIdx.x / G;
 	const Slot S{lds + qw * Grp<G>::kSlotWords};
@@ -306,7 +307,7 @@ __device__ __forceinline__ uint32_t* coal_addr(uint32_t* wslots, int lane, int i
 	return wslots + (w >> 7) * kQuadWords + kRowWords * ((w >> 5) & 3) + (w & 31);
 }
 
-__global__ __launch_bounds__(kScThreads, 2) void sc_fold_coal(ScArgs A) {
+__global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_coal(ScArgs A) {
 	extern __shared__ uint32_t lds[];
 	const int l = threadIdx.x & 3, qw = threadIdx.x >> 2, lane = threadIdx.x & 63;
 	const Slot S{lds + qw * kQuadWords};
@@ -425,7 +426,15 @@ int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 		for (int a = 0; a < 4; a++) A.kcol[k][a] = (uint32_t)tw_mul((uint64_t)k, 1ull << a, 2);
 	// one item per lane group: fold (column, pair), messages (pair, point)
 	const size_t items = fold ? (size_t)sc->d * A.n_pairs : A.n_pairs * (size_t)(A.kmax + 1 - A.skip1);
-	const bool hex = items <= kHexMaxItems;
+	size_t hex_max = kHexMaxItems, post_max = kPostInKernelMaxWG;
+#ifdef BN_DEV
+	{
+		static const char *eh = getenv("BN_SC_HEX_MAX"), *ep = getenv("BN_SC_POST_MAX");
+		if (eh) hex_max = (size_t)atol(eh);
+		if (ep) post_max = (size_t)atol(ep);
+	}
+#endif
+	const bool hex = items <= hex_max;
 	const size_t per_wg = hex ? Grp<16>::kGroups : Grp<4>::kGroups;
 	const size_t grid = (items + per_wg - 1) / per_wg;
 	void* args[] = {&A};
@@ -435,7 +444,7 @@ int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 		 {coal ? (const void*)sc_fold_coal : (const void*)sc_fold<0, 4>, (const void*)sc_fold<1, 4>, (const void*)sc_fold<2, 4>}},
 		{{(const void*)sc_messages<0, 16>, (const void*)sc_messages<1, 16>, (const void*)sc_messages<2, 16>},
 		 {(const void*)sc_fold<0, 16>, (const void*)sc_fold<1, 16>, (const void*)sc_fold<2, 16>}}};
-	A.post = grid <= kPostInKernelMaxWG;
+	A.post = grid <= post_max;
 	BN_HIP(hipLaunchKernel(fns[hex][fold ? 1 : 0][A.mode], dim3((unsigned)grid), dim3(kScThreads), args,
 						   hex ? lds_bytes<16>() : lds_bytes<4>(), sc->stream));
 	if (!fold && !A.post) BN_HIP(hipLaunchKernel((const void*)sc_post, dim3(1), dim3(64), args, 0, sc->stream));
