@@ -240,6 +240,13 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_messages(ScArgs A) {
 			atomicXor(A.acc + (blockIdx.x % kAccCopies) * kAccStride + threadIdx.x, accL[threadIdx.x]);
 		return;  // sc_post follows
 	}
+	if (gridDim.x == 1) {  // a single workgroup posts its own sums
+		if (threadIdx.x < 4 * (A.kmax + 1)) A.res[threadIdx.x] = accL[threadIdx.x];
+		__threadfence_system();
+		__syncthreads();
+		if (threadIdx.x == 0) __hip_atomic_store(A.res + kResSeq, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+		return;
+	}
 	// small grids: the last workgroup to finish reduces the copies and posts the points itself
 	if (threadIdx.x < 4 * (A.kmax + 1) && accL[threadIdx.x]) {
 		// a returning atomic: its value is back only once the XOR has been performed, which
@@ -287,8 +294,9 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold(ScArgs A) {
 #endif
 		grp_mul<G, true>(S, R, l);
 		if (l >= 4) return;
-		// lo is re-read (cache-resident) rather than kept live across the product
-		load_pair<MODE>(A, j, p, l, lo, hi, emask);
+		// lo is re-read (cache-resident) rather than kept live across the quad product; the hex
+		// product leaves the registers for it
+		if constexpr (G == 4) load_pair<MODE>(A, j, p, l, lo, hi, emask);
 		sld(hi, S, l);
 #pragma unroll
 		for (int i = 0; i < 32; i++) lo[i] = (lo[i] ^ hi[i]) & emask;
