@@ -47,6 +47,21 @@ def test_sumcheck_transcript_matches_oracle(n, d, transposed, dev):
     sc.close()
 
 
+def test_sumcheck_transcript_quad_path(dev):
+    # n = 18, d = 3: the first rounds are big enough for the throughput kernels (quad products,
+    # the coalesced fold, the separate post kernel); the smaller cases above run the 16-lane ones
+    n, d = 18, 3
+    ev, ch = _case(n, d, 1818)
+    bs = O.bitslice128(ev)
+    want_s, want_p = O.sumcheck_run(bs, n, d, 1, ch)
+    sc = B.Sumcheck(n, d, True, bs)
+    got_s, got_p = _transcript(sc, n, ch)
+    for r in range(n + 1):
+        assert np.array_equal(got_s[r], want_s[r]), "round %d sum" % r
+        assert np.array_equal(got_p[r], want_p[r]), "round %d points" % r
+    sc.close()
+
+
 @pytest.mark.parametrize("n,d", [(16, 3), (14, 4), (15, 2)])
 def test_sumcheck_protocol_checks(n, d, dev):
     # the reference test's verifier loop (test.cu:31-100) on a bitsliced input
