@@ -16,6 +16,10 @@ with its status. Under torch.distributed every rank drives one GPU:
     synchronize and the max over ranks is reported;
   * c5.batched_ntt: 256 x 2^20-point transforms split over the ranks (rank g owns a contiguous
     slice, no collective; strong scaling over the fixed batch);
+  * configs (world 1 only): BASELINE.json configs 2-4 through tools/bench_configs.py -- the
+    GF(2^128) multiply repeat loops, the 2^20-point NTT, and the 2^24-eval d = 3 sumcheck with
+    bitsliced input and with compact input (memcpy / transpose / raw, the reference harness's
+    phases);
   * c5.sumcheck: the 2^28-evaluation, d = 3 bitsliced sumcheck sharded by 32-element batch
     (b mod world == rank); every round all-gathers the (d + 2) x 16 B partial messages and XORs
     them (RCCL has no XOR reduction); the endgame gathers the last batches.
@@ -46,6 +50,7 @@ def parse():
     ap.add_argument("--log-h", type=int, default=24)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-c5", action="store_true", help="skip the config-5 legs")
+    ap.add_argument("--no-configs", action="store_true", help="skip the configs 2-4 leg (world 1 only)")
     ap.add_argument("--c5-log-n", type=int, default=20)
     ap.add_argument("--c5-batch", type=int, default=256)
     ap.add_argument("--c5-steps", type=int, default=3)
@@ -219,8 +224,13 @@ def main():
     for _ in range(max(5, min(a.steps, 20))):
         ntt.forward_device(d_in, d_out, stream=stream)
     torch.cuda.synchronize(dev)
-    pass_ms = ntt.event_timing()
+    pass_ms_inloop = ntt.event_timing()
     ntt.set_event_timing(False)
+    # steady-state duration per launch of each pass: the pass launched back to back between two
+    # events only (bn_antt_time_passes), so no event sits between the timed launches; d_out is
+    # scratch here and is overwritten by the timed loop below
+    pass_ms = ntt.time_passes(d_in, d_out, reps=max(10, min(a.steps, 40)), stream=stream)
+    torch.cuda.synchronize(dev)
 
     dt = timed(lambda: ntt.forward_device(d_in, d_out, stream=stream), a.steps)
     ms_step = dt / a.steps * 1e3
@@ -271,6 +281,8 @@ def main():
                 "kernel": "pass %s of %d" % (dom, len(pass_ms)),
                 "kernel_ms": dom_ms,
                 "pass_ms": pass_ms,
+                "pass_ms_source": "each pass launched back to back between two hipEvents (bn_antt_time_passes)",
+                "pass_ms_inloop": pass_ms_inloop,
                 "transform_frac": transform_gbps / HBM_PEAK_GBPS,
                 # the pass kernels are VALU-issue bound
                 "limiter": "valu-issue",
@@ -367,8 +379,13 @@ def main():
         del shard
         torch.cuda.empty_cache()
 
+    configs = None
+    if world == 1 and not a.no_configs:
+        configs = configs_leg(dev)
+
     if rank == 0:
         res["c5"] = c5
+        res["configs"] = configs
         if world == 1:
             res["apply_e2e"] = apply_e2e(B, ntt, n)
         res["cpu_baseline"] = cpu_baseline() if (not a.no_cpu and world == 1) else None
@@ -376,6 +393,22 @@ def main():
         json_out.flush()
     if world > 1:
         dist.destroy_process_group()
+
+
+def configs_leg(dev):
+    """BASELINE.json configs 2-4 on this GPU (lines as tools/bench_configs.py prints them), each
+    with its roofline fraction: algorithmic HBM bytes for the NTT and the sumcheck."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_configs as C
+    lines = []
+    C.c2(dev, lines.append)
+    C.ntt_line(dev, lines.append, "c3", 20, 1)
+    C.c4(dev, lines.append, 24, [3])
+    C.c4_phases(dev, lines.append, 24, 3)
+    for ln in lines:
+        if "hbm_gbps_algorithmic" in ln:
+            ln["hbm_frac_algorithmic"] = ln["hbm_gbps_algorithmic"] / HBM_PEAK_GBPS
+    return lines
 
 
 def apply_e2e(B, ntt, n, reps=3):

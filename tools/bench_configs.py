@@ -111,6 +111,44 @@ def c4(dev, out, nvars, ds):
              "hbm_gbps_algorithmic": 3.0 * d * 16 * (1 << nvars) / dt / 1e9})
 
 
+def c4_phases(dev, out, nvars, d, runs=3):
+    """The reference's sumcheck benchmark shape (src/ulvt/sumcheck/bench/benchmark.cu:12-46):
+    DATA_IS_TRANSPOSED = false, timed as memcpy (compact host evals -> HBM), transpose (prover
+    construction from the compact device columns: copy + bitslice transpose on the device) and raw
+    (all rounds + the final messages); medians of `runs` after one warm-up."""
+    import torch
+    import binius_ntt_amd as B
+    g = np.random.default_rng(0x5CF0 + d)
+    host = g.integers(0, 2**32, size=4 * (1 << nvars) * d, dtype=np.uint64).astype(np.uint32).view(np.int32)
+    ch = g.integers(0, 2**32, size=(nvars, 4), dtype=np.uint64).astype(np.uint32)
+    res = []
+    for it in range(runs + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev = torch.from_numpy(host).to(dev)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        sc = B.Sumcheck(nvars, d, False, ev)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        for r in range(nvars):
+            sc.this_round_messages()
+            sc.move_to_next_round(ch[r])
+        sc.this_round_messages()
+        t3 = time.perf_counter()
+        sc.close()
+        del ev
+        if it:
+            res.append((t1 - t0, t2 - t1, t3 - t2))
+    torch.cuda.empty_cache()
+    med = [sorted(x)[len(x) // 2] * 1e3 for x in zip(*res)]
+    out({"config": "c4", "workload": "sumcheck GF(2^128), 2^%d evals, d=%d, compact input "
+                                     "(DATA_IS_TRANSPOSED=false): memcpy / transpose / raw" % (nvars, d),
+         "memcpy_ms": med[0], "transpose_ms": med[1], "raw_ms": med[2], "total_ms": sum(med),
+         "value": (1 << nvars) / (med[2] * 1e-3), "unit": "evals/s (raw)", "runs": runs,
+         "memcpy_note": "pageable numpy -> HBM (torch .to)"})
+
+
 def c5_sumcheck_single(dev, out, nvars=28, d=3):
     """The whole 2^28-eval d=3 sumcheck on ONE GPU (12.9 GB of columns, fits in 288 GB)."""
     import torch
@@ -219,6 +257,8 @@ def main():
         ntt_line(dev, out, "c3", 20, 1)
     if "c4" in only:
         c4(dev, out, a.sc_vars, [int(x) for x in a.sc_d.split(",")])
+        for d in [int(x) for x in a.sc_d.split(",")]:
+            c4_phases(dev, out, a.sc_vars, d)
     if "c5" in only:
         ntt_line(dev, out, "c5 (per-GPU share)", 20, 32)
         c5_sumcheck_shard(dev, out)
