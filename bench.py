@@ -405,9 +405,28 @@ def configs_leg(dev):
     C.ntt_line(dev, lines.append, "c3", 20, 1)
     C.c4(dev, lines.append, 24, [3])
     C.c4_phases(dev, lines.append, 24, 3)
+    # config 2 is VALU-bound (register-resident operands, no HBM traffic): its roofline is the
+    # VALU issue peak, with the kernels' wave-instruction counts per launch from the committed
+    # PMC pass of the same launches (profiles/r02/pmc_c2.json, tools/pmc.sh)
+    pmc = {}
+    try:
+        with open(os.path.join(ROOT, "profiles", "r02", "pmc_c2.json")) as f:
+            pmc = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        pass
+    kern = {"compact": "bn::k_repeat_compact", "multiply_unrolled": "bn::k_repeat_bitsliced",
+            "quad-lane": "bn::k_repeat_quad"}
     for ln in lines:
         if "hbm_gbps_algorithmic" in ln:
             ln["hbm_frac_algorithmic"] = ln["hbm_gbps_algorithmic"] / HBM_PEAK_GBPS
+        if ln.get("config") == "c2":
+            k = next((v for key, v in kern.items() if key in ln["workload"]), None)
+            insts = pmc.get(k, {}).get("SQ_INSTS_VALU") if k else None
+            if insts:
+                rate = insts / (ln["ms"] * 1e-3)
+                ln["valu"] = {"kernel": k, "insts_per_launch": insts, "frac": rate / VALU_PEAK_WAVE_INSTS,
+                              "lane_insts_per_product": insts * 64 / (ln["value"] * ln["ms"] * 1e-3),
+                              "source": "profiles/r02/pmc_c2.json"}
     return lines
 
 

@@ -17,7 +17,7 @@ fi
 if [[ $STEPS == *prof* ]]; then
   export TMPDIR=/tmp
   cd /tmp
-  timeout -k 10 ${PROF_TIMEOUT:-300} rocprofv3 --kernel-trace --stats -f csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --no-cpu --steps 5 --warmup 2 > "$R/gpurun_out/prof.log" 2>&1 || { echo "rocprof failed rc=$?"; tail -30 "$R/gpurun_out/prof.log"; exit 1; }
+  timeout -k 10 ${PROF_TIMEOUT:-300} rocprofv3 --kernel-trace --stats -f csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --no-cpu --no-configs --steps 5 --warmup 2 > "$R/gpurun_out/prof.log" 2>&1 || { echo "rocprof failed rc=$?"; tail -30 "$R/gpurun_out/prof.log"; exit 1; }
   find "$R/gpurun_out/prof" -name "*stats*" | head
 fi
 echo "gpu_check done"

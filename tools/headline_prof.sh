@@ -5,7 +5,7 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"
 mkdir -p gpurun_out
-ARGS=${HP_ARGS:---no-cpu --no-c5 --steps 20 --warmup 3}
+ARGS=${HP_ARGS:---no-cpu --no-c5 --no-configs --steps 20 --warmup 3}
 timeout -k 10 300 python bench.py $ARGS > gpurun_out/hp_bench.json 2> gpurun_out/hp_bench.err || { echo "bench failed"; tail -20 gpurun_out/hp_bench.err; exit 1; }
 cat gpurun_out/hp_bench.json
 export TMPDIR=/tmp
