@@ -204,3 +204,30 @@ def test_point1_from_claim_irregular_call_patterns(n, d, dev):
         if r < n:
             sc.move_to_next_round(ch[r])
     sc.close()
+
+
+def test_prover_from_asynchronous_ntt_output(dev):
+    # the prover is built from a device tensor an NTT is still writing on torch's
+    # current stream (no synchronisation by the caller). The columns are the two transforms of a
+    # batched 2^18-point GF(2^128) NTT (compact, column-major, as DATA_IS_TRANSPOSED = false
+    # wants); the transcript must equal the one of a prover built from the host copy afterwards.
+    import torch
+    n, d = 18, 2
+    x = torch.from_numpy(_rand(4 * (1 << n) * d, 4242).view(np.int32)).to(dev)
+    torch.cuda.synchronize()
+    cols = torch.empty_like(x)
+    ntt = B.AdditiveNTT(B.AdditiveNTTConf(n, 0, B.FanPaarTowerField(7), device=dev.index or 0))
+    for _ in range(4):  # queue several transforms so the last one is surely still running
+        ntt.forward_device(x, cols, batch=d)
+    sc = B.Sumcheck(n, d, False, cols)
+    ch = _rand(4 * n, 4243).reshape(n, 4)
+    got_s, got_p = _transcript(sc, n, ch)
+    sc.close()
+    host = cols.cpu().numpy().view(np.uint32).copy()
+    ref = B.Sumcheck(n, d, False, host)
+    want_s, want_p = _transcript(ref, n, ch)
+    ref.close()
+    assert np.array_equal(got_s, want_s)
+    assert np.array_equal(got_p, want_p)
+    exp = O.antt128(_rand(4 * (1 << n) * d, 4242).reshape(d, 1 << n, 4)[1], n, 0)
+    assert np.array_equal(host.reshape(d, 1 << n, 4)[1], exp)
