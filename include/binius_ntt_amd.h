@@ -223,6 +223,10 @@ int bn_sumcheck_interpolate(const uint32_t* points, int num_points, const uint32
  * src/ulvt/finite_fields/risc0_baby_bear.h:40-190). Elements are uint32_t holding the
  * canonical value (BB31::asUInt32(); inputs are reduced mod p = 15*2^27+1 as BB31(r) does).
  * The transform is the natural-order DFT X[k] = sum_j x[j] w^(jk), w = g^(2^(log_group-log_n)).
+ * Raw risc0 Fp words (Montgomery form, val = x * 2^32 mod p, the bytes of NTTData<BB31> in the
+ * reference) are accepted as well: the transform is linear and multiplies data only by
+ * Montgomery-encoded twiddles, so Montgomery words (< p) in give the reference's Montgomery
+ * words out (tests/test_bb31.py::test_gpu_montgomery_words_in_montgomery_words_out).
  * ------------------------------------------------------------------------------------ */
 typedef struct bn_bb31_ntt_plan bn_bb31_ntt_plan;
 

@@ -111,3 +111,20 @@ def test_gpu_rejects_bad_sizes(dev):
     ntt = B.NTT(B.NTTConfRad2(B.BB31(137), 27, 10))
     with pytest.raises(ValueError):
         ntt.apply(B.NTTData(1 << 9, B.DataOrder.IN_ORDER, 32), B.NTTData(1 << 10))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("log_n", [5, 13, 17, 22])
+def test_gpu_montgomery_words_in_montgomery_words_out(log_n, dev):
+    # risc0 Fp (risc0_baby_bear.h:60-66) keeps val = x * 2^32 mod p in memory, so a raw-buffer
+    # caller passing NTTData<BB31>'s bytes hands over Montgomery words. The transform is linear
+    # and multiplies only by twiddles stored in Montgomery form (one Montgomery product each), so
+    # Montgomery words in give Montgomery words out: the result's bytes equal the reference's.
+    import binius_ntt_amd as B
+    R = (1 << 32) % P
+    x = (O.mt_fill(0x3031 + log_n, 1 << log_n).astype(np.uint64) % P)
+    mont = (x * R % P).astype(np.uint32)
+    ntt = B.NTT(B.NTTConfRad2(B.BB31(137), 27, log_n))
+    got = _dev_run(B, ntt, mont, dev)
+    want = (O.bb31_ntt(x.astype(np.uint32), log_n).astype(np.uint64) * R % P).astype(np.uint32)
+    assert np.array_equal(got, want)
