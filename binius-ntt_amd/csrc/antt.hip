@@ -206,6 +206,12 @@ bool bs_supports(const bn_antt_plan* plan);
 int bs_prepare(bn_antt_plan* plan);
 int bs_time_passes(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, int reps,
                    hipStream_t st, float* ms, int max_passes, int* n_out);
+// Round-scheduled fast path (antt_rd.hip, variant 3): the default when rd_supports(plan).
+bool rd_supports(const bn_antt_plan* plan);
+int rd_prepare(bn_antt_plan* plan);
+int launch_rd(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st);
+int rd_time_passes(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, int reps, hipStream_t st,
+                   float* ms, int max_passes, int* n_out);
 
 }  // namespace bn
 
@@ -245,6 +251,7 @@ extern "C" int bn_antt_plan_create(int device, int field_bits, int log_h, int lo
 	p->variant = 0;
 	if (bs_supports(p)) {
 		int rc = bs_prepare(p);
+		if (rc == BN_OK && rd_supports(p)) rc = rd_prepare(p);
 		if (rc != BN_OK) {
 			hipSetDevice(dev_prev);
 			bn_antt_plan_destroy(p);
@@ -262,6 +269,7 @@ extern "C" int bn_antt_plan_destroy(bn_antt_plan* p) {
 	hipGetDevice(&dev_prev);
 	hipSetDevice(p->device);
 	if (p->s_dev) hipFree(p->s_dev);
+	if (p->rd_tables) hipFree(p->rd_tables);
 	if (p->scratch) hipFree(p->scratch);
 	if (p->h_dev_in) hipFree(p->h_dev_in);
 	if (p->h_dev_out) hipFree(p->h_dev_out);
@@ -280,6 +288,7 @@ extern "C" int bn_antt_plan_destroy(bn_antt_plan* p) {
 static int forward_device_impl(bn_antt_plan* p, const void* d_in, void* d_out, size_t batch, hipStream_t st) {
 	const size_t n_in = ((size_t)1 << p->log_h) * p->limbs;
 	const size_t n_out = n_in << p->log_rate;
+	if (p->variant == 3) return launch_rd(p, (const uint32_t*)d_in, (uint32_t*)d_out, batch, st);
 	if (p->variant != 0) return launch_bs(p, (const uint32_t*)d_in, (uint32_t*)d_out, batch, st);
 	for (size_t b = 0; b < batch; b++) {
 		int rc = launch_v0(p, (const uint32_t*)d_in + b * n_in, (uint32_t*)d_out + b * n_out, st);
@@ -354,13 +363,15 @@ extern "C" int bn_antt_plan_query(const bn_antt_plan* p, int what, int64_t* valu
 
 extern "C" int bn_antt_plan_set_variant(bn_antt_plan* p, int variant) {
 	BN_CHECK_ARG(p != nullptr, "plan is NULL");
-	BN_CHECK_ARG(variant >= 0 && variant <= 2, "variant must be 0, 1 or 2");
-	if (variant != 0 && !bs_supports(p)) BN_FAIL(BN_ERR_UNSUPPORTED, "variants 1 and 2 need log_h >= 12");
+	BN_CHECK_ARG(variant >= 0 && variant <= 3, "variant must be 0, 1, 2 or 3");
+	if (variant != 0 && !bs_supports(p)) BN_FAIL(BN_ERR_UNSUPPORTED, "variants 1-3 need log_h >= 12");
+	if (variant == 3 && !rd_supports(p)) BN_FAIL(BN_ERR_UNSUPPORTED, "variant 3 needs log_rate <= 4");
 	if (variant != 0 && p->variant == 0) {
 		int prev = 0;
 		hipGetDevice(&prev);
 		BN_HIP(hipSetDevice(p->device));
-		const int rc = bs_prepare(p);
+		int rc = bs_prepare(p);
+		if (rc == BN_OK && rd_supports(p)) rc = rd_prepare(p);
 		hipSetDevice(prev);
 		if (rc != BN_OK) return rc;
 	}
@@ -383,12 +394,15 @@ extern "C" int bn_antt_time_passes(bn_antt_plan* p, const void* d_in, void* d_ou
 	BN_CHECK_ARG(p != nullptr && d_in != nullptr && d_out != nullptr && ms_per_pass != nullptr && n_passes != nullptr,
 	             "NULL argument");
 	BN_CHECK_ARG(batch >= 1 && reps >= 1, "batch and reps must be >= 1");
-	if (p->variant == 0) BN_FAIL(BN_ERR_UNSUPPORTED, "pass timing is built for kernel variants 1 and 2");
+	if (p->variant == 0) BN_FAIL(BN_ERR_UNSUPPORTED, "pass timing is built for kernel variants 1-3");
 	int dev_prev = 0;
 	hipGetDevice(&dev_prev);
 	if (dev_prev != p->device) BN_HIP(hipSetDevice(p->device));
-	const int rc = bs_time_passes(p, (const uint32_t*)d_in, (uint32_t*)d_out, batch, reps, (hipStream_t)stream,
-	                              ms_per_pass, max_passes, n_passes);
+	const int rc = p->variant == 3
+	                   ? rd_time_passes(p, (const uint32_t*)d_in, (uint32_t*)d_out, batch, reps, (hipStream_t)stream,
+	                                    ms_per_pass, max_passes, n_passes)
+	                   : bs_time_passes(p, (const uint32_t*)d_in, (uint32_t*)d_out, batch, reps, (hipStream_t)stream,
+	                                    ms_per_pass, max_passes, n_passes);
 	if (dev_prev != p->device) hipSetDevice(dev_prev);
 	return rc;
 }

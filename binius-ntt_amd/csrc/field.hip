@@ -3,6 +3,8 @@
 // repeat-loop microbenchmarks (config 2).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "common.hpp"
 #include "field_dev.hpp"
 #include "bitsliced.hpp"
@@ -44,19 +46,42 @@ __global__ __launch_bounds__(256) void k_bitslice(uint32_t* buf, size_t nblk, in
 	}
 }
 
-__global__ __launch_bounds__(256) void k_gf128_mul_bs(const uint32_t* a, const uint32_t* b, uint32_t* o, size_t nblk) {
-	for (size_t blk = blockIdx.x * (size_t)blockDim.x + threadIdx.x; blk < nblk; blk += (size_t)gridDim.x * blockDim.x) {
-		uint32_t x[128], y[128], z[128];
-#pragma unroll
-		for (int i = 0; i < 128; i++) {
-			x[i] = a[128 * blk + i];
-			y[i] = b[128 * blk + i];
+// Bitsliced GF(2^128) products o = a * b, 32 per 128-word block (multiply_unrolled<7>,
+// circuit_generator/unrolled/binary_tower_unrolled7.cu:6), on the quad-lane product of
+// quad_mul.hpp: block b runs on the 4 lanes of one quad (lane l loads limb l of both operands into
+// the quad's LDS slot and stores limb l of the product), so no lane holds more than ~4 x 32 words
+// and the kernel runs at 2 waves/SIMD without spills. Every operand word is read into the slot
+// before any output word is written: alias-safe for o == a or o == b (core.cu:21).
+__global__ __launch_bounds__(256, 2) void k_gf128_mul_bs(const uint32_t* a, const uint32_t* b, uint32_t* o, size_t nblk) {
+	extern __shared__ uint32_t lds[];
+	const int l = threadIdx.x & 3, qw = threadIdx.x >> 2;
+	const quad::Slot S{lds + qw * quad::kQuadWords};
+	const size_t step = (size_t)gridDim.x * 64;
+	size_t blk = (size_t)blockIdx.x * 64 + qw;  // uniform per quad
+	if (blk >= nblk) return;                    // whole quads leave together
+	uint32_t pa[32], pb[32];
+	quad::ld32(pa, a + 128 * blk + 32 * l);
+	quad::ld32(pb, b + 128 * blk + 32 * l);
+	for (;;) {
+		quad::wsync();
+		quad::sst(S, l, pa);
+		quad::sst(S, 4 + l, pb);
+		// the next block's operands are in flight during this block's product (registers: the
+		// product parks its operands in the slot, so 64 VGPRs of prefetch fit at 2 waves/SIMD)
+		const size_t nxt = blk + step;
+		if (nxt < nblk) {
+			quad::ld32(pa, a + 128 * nxt + 32 * l);
+			quad::ld32(pb, b + 128 * nxt + 32 * l);
 		}
-		bs_mul128(x, y, z);
-#pragma unroll
-		for (int i = 0; i < 128; i++) o[128 * blk + i] = z[i];
+		quad::quad_mul<false>(S, nullptr, l);  // row l <- (rows 0..3) * (rows 4..7)
+		uint32_t x[32];
+		quad::sld(x, S, l);
+		quad::st32(o + 128 * blk + 32 * l, x);
+		if (nxt >= nblk) break;
+		blk = nxt;
 	}
 }
+static size_t quad_lds_bytes();
 
 // bitsliced_repeat-style microbenchmarks (src/ulvt/finite_fields/tests/profiling/kernels/
 // bitsliced_repeat.cu:5-32): `iters` dependent products per lane, operands register-resident.
@@ -146,13 +171,33 @@ extern "C" int bn_bitslice_device(void* buf, size_t nblk, int untranspose, void*
 	return BN_OK;
 }
 
-extern "C" int bn_gf128_mul_bitsliced_device(const void* a, const void* b, void* o, size_t nblk, void* stream) {
-	BN_CHECK_ARG(a && b && o, "NULL device pointer");
+// quad-slot LDS (78 KB) above the 64 KB default: the attribute is set on the current device
+// before every launch (cheap, and correct when the caller switches devices)
+static int quad_kernel_attr(const void* fn) {
+	BN_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)quad_lds_bytes()));
+	return BN_OK;
+}
+
+int gf128_mul_bitsliced_launch(const void* a, const void* b, void* o, size_t nblk, hipStream_t st) {
 	if (!nblk) return BN_OK;
-	hipLaunchKernelGGL(k_gf128_mul_bs, dim3(grid_for(nblk, 256)), dim3(256), 0, (hipStream_t)stream,
-					   (const uint32_t*)a, (const uint32_t*)b, (uint32_t*)o, nblk);
+	int rc = quad_kernel_attr((const void*)k_gf128_mul_bs);
+	if (rc != BN_OK) return rc;
+	int dev = 0, cus = 0;
+	BN_HIP(hipGetDevice(&dev));
+	BN_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+	// 64 blocks per work-group, two work-groups per CU resident: a persistent grid (each quad walks
+	// its blocks with the next block's operands prefetched)
+	size_t grid = (nblk + 63) / 64;
+	grid = std::min(grid, (size_t)std::max(cus, 1) * 2);
+	hipLaunchKernelGGL(k_gf128_mul_bs, dim3((unsigned)grid), dim3(256), quad_lds_bytes(), st, (const uint32_t*)a,
+	                   (const uint32_t*)b, (uint32_t*)o, nblk);
 	BN_HIP(hipGetLastError());
 	return BN_OK;
+}
+
+extern "C" int bn_gf128_mul_bitsliced_device(const void* a, const void* b, void* o, size_t nblk, void* stream) {
+	BN_CHECK_ARG(a && b && o, "NULL device pointer");
+	return gf128_mul_bitsliced_launch(a, b, o, nblk, (hipStream_t)stream);
 }
 
 extern "C" int bn_gf128_mul_repeat_device(int kind, void* state, const void* operand, size_t threads, int iters,
@@ -163,12 +208,8 @@ extern "C" int bn_gf128_mul_repeat_device(int kind, void* state, const void* ope
 	if (!threads) return BN_OK;
 	const unsigned grid = (unsigned)((threads + 255) / 256);
 	if (kind == 2) {
-		static bool attr = false;
-		if (!attr) {
-			BN_HIP(hipFuncSetAttribute((const void*)k_repeat_quad, hipFuncAttributeMaxDynamicSharedMemorySize,
-			                           (int)quad_lds_bytes()));
-			attr = true;
-		}
+		int rc = quad_kernel_attr((const void*)k_repeat_quad);
+		if (rc != BN_OK) return rc;
 		hipLaunchKernelGGL(k_repeat_quad, dim3((unsigned)((threads + 63) / 64)), dim3(256), quad_lds_bytes(),
 		                   (hipStream_t)stream, (uint32_t*)state, (const uint32_t*)operand, threads, iters);
 	} else if (kind == 0)

@@ -108,6 +108,8 @@ unsigned grid_for(size_t n) {
 
 using namespace bn;
 
+int gf128_mul_bitsliced_launch(const void* a, const void* b, void* o, size_t nblk, hipStream_t st);  // field.hip
+
 extern "C" int bn_multiply_unrolled(int height, const uint32_t* a, const uint32_t* b, uint32_t* dst) {
 	BN_CHECK_ARG(a && b && dst, "NULL argument");
 	BN_CHECK_ARG(height >= 2 && height <= 7, "height must be in [2, 7] (got %d)", height);
@@ -127,6 +129,9 @@ extern "C" int bn_multiply_unrolled_device(int height, const void* a, const void
 	BN_CHECK_ARG(a && b && dst, "NULL device pointer");
 	BN_CHECK_ARG(height >= 2 && height <= 7, "height must be in [2, 7] (got %d)", height);
 	if (!nblocks) return BN_OK;
+	// <7> (GF(2^128), the sumcheck's product) runs on the quad-lane product, like
+	// bn_gf128_mul_bitsliced_device: one lane per 128-word block spills the 9712-gate circuit
+	if (height == 7) return gf128_mul_bitsliced_launch(a, b, dst, nblocks, (hipStream_t)stream);
 	const void* fns[6] = {(const void*)k_unrolled<2>, (const void*)k_unrolled<3>, (const void*)k_unrolled<4>,
 	                      (const void*)k_unrolled<5>, (const void*)k_unrolled<6>, (const void*)k_unrolled<7>};
 	void* args[] = {&a, &b, &dst, &nblocks};

@@ -141,6 +141,24 @@ def test_multiply_unrolled_device_matches_oracle(h, dev):
 
 
 @pytest.mark.gpu
+def test_multiply_unrolled7_device_quad_path_large(dev):
+    # multiply_unrolled<7> on the device runs on the quad-lane product, a persistent grid of 64-block
+    # work-groups whose quads walk their blocks with the next operands prefetched: a batch of many grid
+    # rounds (and a ragged last one), with the product written over the SECOND operand (alias-safe,
+    # core.cu:21), sampled against the host
+    import torch
+    nblk = 262144 + 77
+    g = np.random.default_rng(77)
+    a = torch.randint(-2**31, 2**31 - 1, (128 * nblk,), dtype=torch.int32, device=dev, generator=None)
+    b = torch.from_numpy(g.integers(0, 2**32, size=128 * nblk, dtype=np.uint64).astype(np.uint32).view(np.int32)).to(dev)
+    a_np, b_np = _np(a).reshape(nblk, 128), _np(b).reshape(nblk, 128)
+    B.multiply_unrolled_device(7, a, b, b)
+    got = _np(b).reshape(nblk, 128)
+    for k in (0, 1, 63, 64, 4095, 262143, 262144, nblk - 1) + tuple(g.integers(0, nblk, size=24)):
+        assert np.array_equal(got[k], B.multiply_unrolled(7, a_np[k], b_np[k])), k
+
+
+@pytest.mark.gpu
 def test_packed32_device_kats(field_kats, dev):
     import torch
     for key, h in (("simd_h0", 0), ("simd_h2", 2), ("simd8", 3), ("simd16", 4), ("simd_h5", 5)):

@@ -87,6 +87,38 @@ def test_gf128_north_star_size_limb_md5_and_oracle(ntt_md5, dev):
     assert np.array_equal(y, O.antt128(x, log_h, 0))
 
 
+@pytest.mark.slow
+def test_c5_batched_256x2p20_at_size(ntt_md5, dev):
+    # BASELINE.json configs[4], one GPU's whole batch in ONE forward_device call: 256 x 2^20
+    # GF(2^128) transforms (4 GiB in, 4 GiB out). Limb 0 of every transform is the reference's
+    # mt19937(0xdeadbeef + 20) stream, so every output limb-0 plane must hash to
+    # additive_ntt_hashes[0][20] (test_ntt.cu:52-124, 191-217); limbs 1..3 are independent random
+    # words per transform, and transforms 0, 127 and 255 are checked in full against the oracle.
+    import hashlib
+    import torch
+    log_h, batch = 20, 256
+    n = 1 << log_h
+    limb0 = torch.from_numpy(O.mt_fill(0xDEADBEEF + log_h, n).view(np.int32)).to(dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0xC5)
+    x = torch.randint(-2**31, 2**31 - 1, (batch, n, 4), dtype=torch.int32, device=dev, generator=g)
+    x[:, :, 0] = limb0
+    y = torch.empty_like(x)
+    ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(7)))
+    ntt.forward_device(x.view(-1), y.view(-1), batch=batch)
+    torch.cuda.synchronize()
+    want_md5 = ntt_md5["0"][log_h]
+    planes = y[:, :, 0].contiguous().cpu().numpy().view(np.uint32)
+    bad = [b for b in range(batch) if hashlib.md5(planes[b].tobytes()).hexdigest() != want_md5]
+    assert not bad, "limb-0 MD5 differs from the reference table for transforms %s" % bad[:16]
+    del planes
+    for b in (0, 127, 255):
+        xb = x[b].cpu().numpy().view(np.uint32)
+        want = np.zeros_like(xb)
+        O.lib().orc_antt128_limbwise_mt(xb.reshape(-1), want.reshape(-1), log_h, 0, O.threads())
+        assert np.array_equal(y[b].cpu().numpy().view(np.uint32), want), "transform %d differs from the oracle" % b
+
+
 def test_gf128_linearity_at_2_20(dev):
     # size-independent property: NTT(a ^ b) == NTT(a) ^ NTT(b)
     log_h = 20

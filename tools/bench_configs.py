@@ -51,8 +51,13 @@ def c2(dev, out):
     import binius_ntt_amd as B
     st = torch.cuda.current_stream(dev)
     g = np.random.default_rng(2)
-    for kind, name, words, per in ((0, "compact", 4, 1), (1, "bitsliced, multiply_unrolled<7> per lane", 128, 32),
-                                   (2, "bitsliced, quad-lane product", 128, 32)):
+    # kind 2 is the product behind the boundary's multiply_unrolled<7> (bn_multiply_unrolled_device(7),
+    # bn_gf128_mul_bitsliced_device); kind 1 keeps the reference's structure (one 32-product block
+    # per lane, binary_tower_unrolled7.cu) for comparison only
+    for kind, name, words, per in ((0, "compact", 4, 1),
+                                   (2, "bitsliced multiply_unrolled<7>, quad-lane product (the boundary's path)", 128, 32),
+                                   (1, "bitsliced, one 9712-gate multiply_unrolled<7> circuit per lane (reference "
+                                       "structure, not the boundary's path)", 128, 32)):
         threads = 256 * 2048 if kind == 0 else 256 * 1024
         iters = 2000 if kind == 0 else 20 if kind == 1 else 200
         state = torch.from_numpy(g.integers(0, 2**32, size=threads * words, dtype=np.uint64).astype(np.uint32)
@@ -63,6 +68,18 @@ def c2(dev, out):
         prods = threads * iters * per
         out({"config": "c2", "workload": "GF(2^128) multiply repeat loop, %s" % name, "value": prods / (ms * 1e-3),
              "unit": "products/s", "ms": ms, "threads": threads, "iters": iters})
+    # the boundary entry itself on HBM-resident operands: dst = a * b over 2^20 blocks (32 Mi products;
+    # 48 B of HBM traffic per product: two operands read, one product written)
+    nblk = 1 << 20
+    a = torch.from_numpy(g.integers(0, 2**32, size=128 * nblk, dtype=np.uint64).astype(np.uint32).view(np.int32)).to(dev)
+    b = torch.from_numpy(g.integers(0, 2**32, size=128 * nblk, dtype=np.uint64).astype(np.uint32).view(np.int32)).to(dev)
+    o = torch.empty_like(a)
+    ms = ev_time(lambda: B.multiply_unrolled_device(7, a, b, o, stream=st), 5, st)
+    prods = 32 * nblk
+    out({"config": "c2", "workload": "GF(2^128) bitsliced products through bn_multiply_unrolled_device(7), 2^20 "
+                                     "HBM-resident 128-word blocks", "value": prods / (ms * 1e-3), "unit": "products/s",
+         "ms": ms, "hbm_gbps_algorithmic": 3 * 512.0 * nblk / (ms * 1e-3) / 1e9})
+    del a, b, o
 
 
 def ntt_line(dev, out, cfg, log_h, batch):
