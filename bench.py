@@ -58,6 +58,10 @@ def parse():
     ap.add_argument("--sc-d", type=int, default=3)
     ap.add_argument("--sc-runs", type=int, default=2)
     ap.add_argument("--variant", type=int, default=None, help="NTT kernel variant (default: the plan's choice)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the launch path: the --gpus relaunch, process-group setup (gloo), "
+                         "barriers, max-over-ranks timing, batch slicing and the sharded message exchange, "
+                         "with no GPU work; prints one JSON line")
     return ap.parse_args()
 
 
@@ -132,6 +136,26 @@ def cpu_baseline():
             "cpu_model": model, "nproc": nproc, "cpus_allowed": allowed, "per_size": per_size}
 
 
+def limb0_check(d_out, log_h):
+    """MD5 of the timed loop's output limb-0 plane against the reference table entry (the golden
+    data file tests/golden/additive_ntt_md5.json holds test_ntt.cu:52-124 as data)."""
+    import hashlib
+    import numpy as np
+    plane = d_out.view(-1, 4)[:, 0].contiguous().cpu().numpy().view(np.uint32)
+    got = hashlib.md5(plane.tobytes()).hexdigest()
+    want = None
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "additive_ntt_md5.json")) as f:
+            want = json.load(f)["hashes"]["0"][log_h] or None  # list indexed by log_h
+    except (OSError, ValueError, KeyError, IndexError):
+        pass
+    ok = want is not None and got == want
+    if want is not None and not ok:
+        print("bench.py: OUTPUT MISMATCH: limb-0 MD5 %s != reference %s" % (got, want), file=sys.stderr)
+    return {"limb0_md5": got, "reference_md5": want, "match": ok,
+            "source": "additive_ntt_hashes[0][%d] (src/ulvt/ntt/tests/test_ntt.cu:52-124)" % log_h}
+
+
 def load_pass_counters(log_h):
     """SQ_INSTS_VALU per launch of each pass from the committed rocprofv3 PMC summary, keyed
     by log_h and pass index (tools/pmc_summary.py); None if this layout was not profiled."""
@@ -153,9 +177,46 @@ def load_traffic(log_h):
         return None
 
 
+def dry_run(a, json_out):
+    """--dry-run: everything of the multi-rank path that does not need a GPU (tests/test_bench_cli.py)."""
+    import numpy as np
+    import torch.distributed as dist
+    from binius_ntt_amd import distributed as D
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+    res = {"dry_run": True, "n_gpus": world, "rank_checks": []}
+    if world > 1:
+        dist.barrier()
+        ex = D.WordExchange(4 * (a.sc_d + 2))
+        mine = np.random.default_rng(rank).integers(0, 2**32, size=ex.n, dtype=np.uint64).astype(np.uint32)
+        want = np.bitwise_xor.reduce(np.stack([np.random.default_rng(r).integers(0, 2**32, size=ex.n, dtype=np.uint64)
+                                               .astype(np.uint32) for r in range(world)]), axis=0)
+        got = ex.xor(mine)
+        t = __import__("torch").tensor([float(rank)], dtype=__import__("torch").float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        lo, hi = D.batch_slice(a.c5_batch, rank, world)
+        sizes = [0] * world
+        dist.all_gather_object(sizes, hi - lo)
+        res["rank_checks"] = {"xor_exchange_ok": bool(np.array_equal(got, want)), "max_over_ranks": t.item(),
+                              "batch_slices_cover": sum(sizes) == a.c5_batch}
+        dist.barrier()
+    if rank == 0:
+        json_out.write(json.dumps(res) + "\n")
+        json_out.flush()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
     relaunch_if_needed(a)
+    if a.dry_run:
+        json_out = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
+        return dry_run(a, json_out)
     # stdout carries exactly one JSON line (rank 0): library chatter (e.g. gloo's connection
     # messages on std::cout) is sent to stderr by pointing fd 1 there for the rest of the run
     json_out = os.fdopen(os.dup(1), "w")
@@ -206,8 +267,14 @@ def main():
     # ---------------- headline: 2^24 GF(2^128) additive NTT, one transform per rank
     log_h = a.log_h
     n = 1 << log_h
-    x = np.random.default_rng(0xDEADBEEF + log_h + rank).integers(0, 2**32, size=4 * n, dtype=np.uint64)
-    d_in = torch.from_numpy(x.astype(np.uint32).view(np.int32)).to(dev)
+    # limb 0 = the reference test's input stream, std::mt19937(0xdeadbeef + log_h) (test_ntt.cu:192-199;
+    # numpy's legacy MT19937 seeding is the same generator), so the output limb-0 plane must hash to
+    # additive_ntt_hashes[0][log_h] (test_ntt.cu:52-124) -- checked after the timed loop; limbs 1..3 =
+    # numpy PCG64 words (independent per rank)
+    x = np.random.default_rng(0xDEADBEEF + log_h + rank).integers(0, 2**32, size=(n, 4), dtype=np.uint64)
+    x = x.astype(np.uint32)
+    x[:, 0] = np.random.RandomState(0xDEADBEEF + log_h).randint(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    d_in = torch.from_numpy(x.reshape(-1).view(np.int32)).to(dev)
     del x
     d_out = torch.empty_like(d_in)
     ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(7), device=local))
@@ -234,6 +301,7 @@ def main():
 
     dt = timed(lambda: ntt.forward_device(d_in, d_out, stream=stream), a.steps)
     ms_step = dt / a.steps * 1e3
+    out_check = limb0_check(d_out, log_h)
     elems_per_s = world * n / (dt / a.steps)
     alg_bytes = 2 * 16 * n  # read input once + write output once
     transform_gbps = alg_bytes / (ms_step * 1e-3) / 1e9
@@ -266,7 +334,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "gf2_128 (u32 limbs, bitwise)",
-            "data": "synthetic (numpy PCG64 seeded limbs)",
+            "data": "synthetic: limb 0 = std::mt19937(0xdeadbeef + log_h) (the reference test stream), limbs 1-3 "
+                    "numpy PCG64",
+            "output_check": out_check,
             "config": {"workload": "additive NTT over GF(2^128), log_h=%d, log_rate=0, one transform per GPU"
                                    % log_h, "log_h": log_h, "log_rate": 0, "field": "GF(2^128)",
                        "kernel_variant": ntt.variant(), "parallelism": "independent transform per rank"},
@@ -335,9 +405,12 @@ def main():
         challenges = rng.integers(0, 2**32, size=(N, 4), dtype=np.uint64).astype(np.uint32)
         group = None
 
+        exch = []
+
         def run_sumcheck(check):
             prover = B.Sumcheck.from_shard(N, d, shard, rank, world, device=local)
             sc = D.ShardedSumcheck(prover, group)
+            exch.append(sc)
             barrier()
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
@@ -368,6 +441,8 @@ def main():
             times.append(el)
             oks.append(ok)
         tsc = sorted(times)[len(times) // 2]
+        last = exch[-1]
+        ex_ms = max_over_ranks(last.exchange_seconds * 1e3)
         alg = sum(d * 16 * ((1 << (N - i)) + (1 << (N - i - 1))) for i in range(N))
         c5["sumcheck"] = {
             "workload": "GF(2^128) sumcheck, 2^%d evals, d=%d, bitsliced, sharded %d ways by 32-element batch; "
@@ -375,7 +450,9 @@ def main():
             "ms": tsc * 1e3, "evals_per_s": (1 << N) / tsc, "runs": len(times),
             "protocol_checks_pass": all(oks),
             "per_gpu_alg_gbps": alg / world / tsc / 1e9,
-            "collective": "all_gather (%s) + XOR" % (backend if world > 1 else "none, world 1")}
+            "collective": "all_gather_into_tensor (%s) + XOR" % (backend if world > 1 else "none, world 1"),
+            "exchange_ms": ex_ms, "exchange_rounds": last.exchange_rounds,
+            "exchange_ms_per_round": ex_ms / last.exchange_rounds if last.exchange_rounds else None}
         del shard
         torch.cuda.empty_cache()
 
@@ -404,7 +481,12 @@ def configs_leg(dev):
     C.c2(dev, lines.append)
     C.ntt_line(dev, lines.append, "c3", 20, 1)
     C.c4(dev, lines.append, 24, [3])
+    # the reference harness's matrix (bench/benchmark.cu:71-85): N = 20 for d = 2..4, N = 24 and
+    # N = 28 at d = 3 (12.9 GB of columns at N = 28: one timed run)
+    for d in (2, 3, 4):
+        C.c4_phases(dev, lines.append, 20, d)
     C.c4_phases(dev, lines.append, 24, 3)
+    C.c4_phases(dev, lines.append, 28, 3, runs=1)
     # config 2 is VALU-bound (register-resident operands, no HBM traffic): its roofline is the
     # VALU issue peak, with the kernels' wave-instruction counts per launch from the committed
     # PMC pass of the same launches (profiles/r02/pmc_c2.json, tools/pmc.sh)

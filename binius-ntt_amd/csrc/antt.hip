@@ -7,6 +7,7 @@
 // 2^(stage+1) elements, with twiddle w = XOR_k s[stage][k] over the set bits k of
 // (c << (log_h-1-stage)) | blk (calculate_twiddle, :59-77). Output is coset-major.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -238,13 +239,13 @@ extern "C" int bn_antt_plan_create(int device, int field_bits, int log_h, int lo
 	p->width = log_h + log_rate - 1;
 	subspace_evals(log_h, log_rate, p->s_host);
 	int dev_prev = 0;
-	hipGetDevice(&dev_prev);
+	(void)hipGetDevice(&dev_prev);
 	hipError_t e = hipSetDevice(device);
 	if (e == hipSuccess) e = hipMalloc(&p->s_dev, std::max<size_t>(p->s_host.size(), 1) * sizeof(uint32_t));
 	if (e == hipSuccess && !p->s_host.empty())
 		e = hipMemcpy(p->s_dev, p->s_host.data(), p->s_host.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
 	if (e != hipSuccess) {
-		hipSetDevice(dev_prev);
+		(void)hipSetDevice(dev_prev);
 		bn_antt_plan_destroy(p);
 		BN_FAIL(BN_ERR_HIP, "plan allocation failed: %s", hipGetErrorString(e));
 	}
@@ -252,13 +253,18 @@ extern "C" int bn_antt_plan_create(int device, int field_bits, int log_h, int lo
 	if (bs_supports(p)) {
 		int rc = bs_prepare(p);
 		if (rc == BN_OK && rd_supports(p)) rc = rd_prepare(p);
+		// BN_ANTT_VARIANT=1|2|3 overrides the default fast-path kernel for new plans (A/B runs)
+		if (rc == BN_OK && getenv("BN_ANTT_VARIANT")) {
+			const int v = atoi(getenv("BN_ANTT_VARIANT"));
+			if ((v == 1 || v == 2) || (v == 3 && rd_supports(p))) p->variant = v;
+		}
 		if (rc != BN_OK) {
-			hipSetDevice(dev_prev);
+			(void)hipSetDevice(dev_prev);
 			bn_antt_plan_destroy(p);
 			return rc;
 		}
 	}
-	hipSetDevice(dev_prev);
+	(void)hipSetDevice(dev_prev);
 	*out = p;
 	return BN_OK;
 }
@@ -266,21 +272,21 @@ extern "C" int bn_antt_plan_create(int device, int field_bits, int log_h, int lo
 extern "C" int bn_antt_plan_destroy(bn_antt_plan* p) {
 	if (!p) return BN_OK;
 	int dev_prev = 0;
-	hipGetDevice(&dev_prev);
-	hipSetDevice(p->device);
-	if (p->s_dev) hipFree(p->s_dev);
-	if (p->rd_tables) hipFree(p->rd_tables);
-	if (p->scratch) hipFree(p->scratch);
-	if (p->h_dev_in) hipFree(p->h_dev_in);
-	if (p->h_dev_out) hipFree(p->h_dev_out);
+	(void)hipGetDevice(&dev_prev);
+	(void)hipSetDevice(p->device);
+	if (p->s_dev) (void)hipFree(p->s_dev);
+	if (p->rd_tables) (void)hipFree(p->rd_tables);
+	if (p->scratch) (void)hipFree(p->scratch);
+	if (p->h_dev_in) (void)hipFree(p->h_dev_in);
+	if (p->h_dev_out) (void)hipFree(p->h_dev_out);
 	for (const auto& q : p->pending) {
-		hipEventSynchronize(q.end);
-		hipEventDestroy(q.begin);
-		hipEventDestroy(q.end);
+		(void)hipEventSynchronize(q.end);
+		(void)hipEventDestroy(q.begin);
+		(void)hipEventDestroy(q.end);
 	}
-	for (auto e : p->ev_pool) hipEventDestroy(e);
-	if (p->own_stream) hipStreamDestroy(p->own_stream);
-	hipSetDevice(dev_prev);
+	for (auto e : p->ev_pool) (void)hipEventDestroy(e);
+	if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
+	(void)hipSetDevice(dev_prev);
 	delete p;
 	return BN_OK;
 }
@@ -307,10 +313,10 @@ extern "C" int bn_antt_forward_device(bn_antt_plan* p, const void* d_in, void* d
 	const char* b = (const char*)d_out;
 	BN_CHECK_ARG(a + in_bytes <= b || b + out_bytes <= a, "d_in and d_out must not overlap");
 	int dev_prev = 0;
-	hipGetDevice(&dev_prev);
+	(void)hipGetDevice(&dev_prev);
 	if (dev_prev != p->device) BN_HIP(hipSetDevice(p->device));
 	int rc = forward_device_impl(p, d_in, d_out, batch, (hipStream_t)stream);
-	if (dev_prev != p->device) hipSetDevice(dev_prev);
+	if (dev_prev != p->device) (void)hipSetDevice(dev_prev);
 	return rc;
 }
 
@@ -320,7 +326,7 @@ extern "C" int bn_antt_forward_host(bn_antt_plan* p, const void* in, size_t in_e
 	BN_CHECK_ARG(in != nullptr && out != nullptr, "host buffers must be non-NULL");
 	BN_CHECK_ARG(in_elems == ((size_t)1 << p->log_h), "input has %zu elements, plan expects 2^%d", in_elems, p->log_h);
 	int dev_prev = 0;
-	hipGetDevice(&dev_prev);
+	(void)hipGetDevice(&dev_prev);
 	BN_HIP(hipSetDevice(p->device));
 	const size_t in_bytes = in_elems * p->limbs * 4;
 	const size_t out_bytes = in_bytes << p->log_rate;
@@ -332,12 +338,12 @@ extern "C" int bn_antt_forward_host(bn_antt_plan* p, const void* in, size_t in_e
 	BN_HIP(hipMemcpyAsync(p->h_dev_in, in, in_bytes, hipMemcpyHostToDevice, p->own_stream));
 	int rc = forward_device_impl(p, p->h_dev_in, p->h_dev_out, 1, p->own_stream);
 	if (rc != BN_OK) {
-		hipSetDevice(dev_prev);
+		(void)hipSetDevice(dev_prev);
 		return rc;
 	}
 	BN_HIP(hipMemcpyAsync(out, p->h_dev_out, out_bytes, hipMemcpyDeviceToHost, p->own_stream));
 	BN_HIP(hipStreamSynchronize(p->own_stream));
-	hipSetDevice(dev_prev);
+	(void)hipSetDevice(dev_prev);
 	return BN_OK;
 }
 
@@ -368,11 +374,16 @@ extern "C" int bn_antt_plan_set_variant(bn_antt_plan* p, int variant) {
 	if (variant == 3 && !rd_supports(p)) BN_FAIL(BN_ERR_UNSUPPORTED, "variant 3 needs log_rate <= 4");
 	if (variant != 0 && p->variant == 0) {
 		int prev = 0;
-		hipGetDevice(&prev);
+		(void)hipGetDevice(&prev);
 		BN_HIP(hipSetDevice(p->device));
 		int rc = bs_prepare(p);
 		if (rc == BN_OK && rd_supports(p)) rc = rd_prepare(p);
-		hipSetDevice(prev);
+		// BN_ANTT_VARIANT=1|2|3 overrides the default fast-path kernel for new plans (A/B runs)
+		if (rc == BN_OK && getenv("BN_ANTT_VARIANT")) {
+			const int v = atoi(getenv("BN_ANTT_VARIANT"));
+			if ((v == 1 || v == 2) || (v == 3 && rd_supports(p))) p->variant = v;
+		}
+		(void)hipSetDevice(prev);
 		if (rc != BN_OK) return rc;
 	}
 	p->variant = variant;
@@ -396,14 +407,14 @@ extern "C" int bn_antt_time_passes(bn_antt_plan* p, const void* d_in, void* d_ou
 	BN_CHECK_ARG(batch >= 1 && reps >= 1, "batch and reps must be >= 1");
 	if (p->variant == 0) BN_FAIL(BN_ERR_UNSUPPORTED, "pass timing is built for kernel variants 1-3");
 	int dev_prev = 0;
-	hipGetDevice(&dev_prev);
+	(void)hipGetDevice(&dev_prev);
 	if (dev_prev != p->device) BN_HIP(hipSetDevice(p->device));
 	const int rc = p->variant == 3
 	                   ? rd_time_passes(p, (const uint32_t*)d_in, (uint32_t*)d_out, batch, reps, (hipStream_t)stream,
 	                                    ms_per_pass, max_passes, n_passes)
 	                   : bs_time_passes(p, (const uint32_t*)d_in, (uint32_t*)d_out, batch, reps, (hipStream_t)stream,
 	                                    ms_per_pass, max_passes, n_passes);
-	if (dev_prev != p->device) hipSetDevice(dev_prev);
+	if (dev_prev != p->device) (void)hipSetDevice(dev_prev);
 	return rc;
 }
 

@@ -108,28 +108,6 @@ __device__ __forceinline__ void mul_tw(int field, const uint32_t* x, const uint3
 	}
 }
 
-// out = t*x for 32 bitsliced GF(2^32) limbs and a per-lane scalar twiddle t (same field rules as
-// mul_tw): the twiddle's Karatsuba w-side leaves are packed bits (bsmN_wpack) extracted at their
-// use, so no 32-word broadcast array is live during the circuit (~40 fewer VGPRs).
-template <int FMAX>
-__device__ __forceinline__ void mul_tw_packed(int field, const uint32_t* x, uint32_t t, uint32_t* out) {
-	if (FMAX <= 8 || field <= 8) {
-		uint32_t wp[kBsm3PackWords];
-		bsm3_wpack(t, wp);
-#pragma unroll
-		for (int g = 0; g < 4; g++) bsm3_mulpk(x + 8 * g, wp, out + 8 * g);
-	} else if (FMAX <= 16 || field <= 16) {
-		uint32_t wp[kBsm4PackWords];
-		bsm4_wpack(t, wp);
-#pragma unroll
-		for (int g = 0; g < 2; g++) bsm4_mulpk(x + 16 * g, wp, out + 16 * g);
-	} else {
-		uint32_t wp[kBsm5PackWords];
-		bsm5_wpack(t, wp);
-		bsm5_mulpk(x, wp, out);
-	}
-}
-
 // LDS image of a tile: one plane per limb, block q of limb l at l*kPlane + q*kLimbStride (stride 36
 // words: 16 consecutive blocks of one plane hit 16 distinct 4-bank groups, so a wave's
 // ds_read_b128 over consecutive blocks is conflict-free).
@@ -240,6 +218,9 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 #pragma unroll
 			for (int i = 0; i < 32; i++) Pr[i] = V[i] ^ W[i];
 		} else {
+			// V complete before the circuit: with its loads in flight the scheduler hoists the w-side
+			// Karatsuba sums to cover their latency, and runs out of registers
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 			__builtin_amdgcn_sched_barrier(0);
 			mul_tw<FMAX>(ps.field[j], V, W, Pr);  // sub-field circuits reuse W: Pr must not alias it
 			__builtin_amdgcn_sched_barrier(0);
@@ -377,6 +358,7 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 #pragma unroll
 					for (int i = 0; i < 32; i++) T[i] ^= W[i];
 				} else {
+					asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // operands complete (see block_stage)
 					__builtin_amdgcn_sched_barrier(0);
 					mul_tw<FMAX>(ps.field[s], T, W, T);
 					__builtin_amdgcn_sched_barrier(0);
@@ -663,6 +645,19 @@ static int launch_one(bn_antt_plan* plan, const BsPass& pass, int i, const uint3
 	return BN_OK;
 }
 
+// pass i of variant 1 alone (variant 3 runs its bottom pass through this kernel: same pass split,
+// same HBM layouts)
+int bs_launch_pass(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st) {
+	size_t n_passes = 0;
+	const BsPass* passes = bs_passes(plan, &n_passes);
+	if (i < 0 || (size_t)i >= n_passes) BN_FAIL(BN_ERR_INVALID, "pass %d out of range", i);
+	const int saved = plan->variant;
+	plan->variant = 1;
+	const int rc = launch_one(plan, passes[i], i, d_in, d_out, batch, st, dev_knobs());
+	plan->variant = saved;
+	return rc;
+}
+
 int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st) {
 	size_t n_passes = 0;
 	const BsPass* passes = bs_passes(plan, &n_passes);
@@ -904,8 +899,6 @@ __global__ __launch_bounds__(64 * L, (RtCfg<ROLE, FMAX>::OCC)) void antt_rt_pass
 #pragma unroll
 			for (int i = 0; i < 32; i += 4) *(uint4*)(park + i) = rt_pack(R0 + i);
 		}
-		// (mul_tw_packed, the packed-leaf form, needs ~40 fewer VGPRs in isolation but measured
-		// slower here: bottom pass block stages 59 k -> 77 k cycles per wave-tile)
 		__builtin_amdgcn_sched_barrier(0);
 		mul_tw<FMAX>(ps.field_m[m], R1, W, Pr);
 		__builtin_amdgcn_sched_barrier(0);

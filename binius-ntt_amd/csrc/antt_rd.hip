@@ -102,6 +102,8 @@ struct RdParams {
 	const uint32_t* src;
 	uint32_t* dst;
 	int log_h, log_rate;
+	int outmode;  // EXPERIMENT
+	int dbg;      // EXPERIMENT: 1 skip in-word stages, 2 skip rounds, 4 skip K=1 rounds
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -136,20 +138,31 @@ __host__ __device__ constexpr uint32_t lane_mask(int j) {
 template <int SW, int FMAX>
 __device__ __forceinline__ void mul_slice(int field, uint32_t t, const uint32_t* v, uint32_t* P) {  // P may be v
 	uint32_t W[32];
+#ifdef RD_EXP_K1ONLY
+	if (FMAX <= 8) {
+#else
 	if (SW == 8 || FMAX <= 8 || field <= 8) {
+#endif
 #pragma unroll
 		for (int b = 0; b < 8; b++) W[b] = (uint32_t)__builtin_amdgcn_sbfe(t, b, 1);
 #pragma unroll
 		for (int g = 0; g < SW / 8; g++) bsm3_mul(v + 8 * g, W, P + 8 * g);
-	} else if (SW == 16 || FMAX <= 16 || field <= 16) {
+	} else if (SW == 16 || FMAX <= 16
+#ifndef RD_EXP_K1ONLY
+	           || field <= 16
+#endif
+	           ) {
 #pragma unroll
 		for (int b = 0; b < 16; b++) W[b] = (uint32_t)__builtin_amdgcn_sbfe(t, b, 1);
 #pragma unroll
 		for (int g = 0; g < SW / 16; g++) bsm4_mul(v + 16 * g, W, P + 16 * g);
 	} else {
+		// operands complete before the circuit: with a load still in flight the scheduler hoists the
+		// w-side Karatsuba sums (up to 243 live leaves) to cover its latency, and spills
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+		__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 		for (int b = 0; b < 32; b++) W[b] = (uint32_t)__builtin_amdgcn_sbfe(t, b, 1);
-		__builtin_amdgcn_sched_barrier(0);
 		bsm5_mul(v, W, P);
 		__builtin_amdgcn_sched_barrier(0);
 	}
@@ -192,18 +205,22 @@ __device__ __forceinline__ void rd_round(const RdRound& R, char* pl, int lane, u
 #pragma unroll
 		for (int c = 0; c < NCH; c++) lds_rd4(pl, A ^ (R.U[1] ^ (16u * c)), Pr + 4 * c);
 		mul_slice<SW, FMAX>(R.fld, tg, Pr, Pr);
+		// all u and old-v reads in flight together (one LDS latency), then the butterfly
+		uint32_t Uo[SW], Vo[SW];
 #pragma unroll
 		for (int c = 0; c < NCH; c++) {
-			uint32_t u4[4], v4[4];
-			lds_rd4(pl, A ^ (R.U[0] ^ (16u * c)), u4);
-			lds_rd4(pl, A ^ (R.U[1] ^ (16u * c)), v4);
+			lds_rd4(pl, A ^ (R.U[0] ^ (16u * c)), Uo + 4 * c);
+			lds_rd4(pl, A ^ (R.U[1] ^ (16u * c)), Vo + 4 * c);
+		}
 #pragma unroll
-			for (int i = 0; i < 4; i++) {
-				u4[i] ^= Pr[4 * c + i];
-				v4[i] ^= u4[i];
-			}
-			lds_wr4(pl, A ^ (R.U[0] ^ (16u * c)), u4);
-			lds_wr4(pl, A ^ (R.U[1] ^ (16u * c)), v4);
+		for (int i = 0; i < SW; i++) {
+			Uo[i] ^= Pr[i];
+			Vo[i] ^= Uo[i];
+		}
+#pragma unroll
+		for (int c = 0; c < NCH; c++) {
+			lds_wr4(pl, A ^ (R.U[0] ^ (16u * c)), Uo + 4 * c);
+			lds_wr4(pl, A ^ (R.U[1] ^ (16u * c)), Vo + 4 * c);
 		}
 		lds_order();
 		return;
@@ -339,13 +356,19 @@ __global__ __launch_bounds__(64 * L, 2) void antt_rd_pass(RdParams P, const RdPa
 
 	// ---- block stages, in rounds (each wave on its own plane)
 	for (int i = 0; i < ps.n_rounds; i++) {
+		if (P.dbg & 2) break;
 		const RdRound& R = ps.rounds[i];
+		if ((P.dbg & 4) && R.k == 1) continue;
+#ifdef RD_EXP_K1ONLY
+		rd_round<1, FMAX>(R, pl, lane, cuv);
+#else
 		if (R.k == 3)
 			rd_round<3, 8>(R, pl, lane, cuv);
 		else if (R.k == 2)
 			rd_round<2, (FMAX < 16 ? FMAX : 16)>(R, pl, lane, cuv);
 		else
 			rd_round<1, FMAX>(R, pl, lane, cuv);
+#endif
 	}
 
 	if (LAST) {
@@ -371,7 +394,7 @@ __global__ __launch_bounds__(64 * L, 2) void antt_rd_pass(RdParams P, const RdPa
 				lds_rd4(yp, bb ^ (16u * c), B + 4 * c);
 			}
 		}
-		for (int s = 4; s >= 0; s--) {
+		for (int s = 4; s >= ((P.dbg & 1) ? 5 : 0); s--) {
 			const int d = 1 << s;
 			const uint32_t um = ~lane_mask(s);  // u-lanes (bit s clear)
 			uint32_t cb = (uint32_t)__builtin_amdgcn_readlane((int)cuv, s);  // bottom pass: lo = 0, j = s
@@ -385,10 +408,18 @@ __global__ __launch_bounds__(64 * L, 2) void antt_rd_pass(RdParams P, const RdPa
 				W[i] = ps.pat[s][i] ^ (uint32_t)__builtin_amdgcn_sbfe(cb, i, 1);
 			}
 			const int f = ps.field[s];
+#ifdef RD_EXP_K1ONLY
+			if (FMAX <= 8) {
+#else
 			if (FMAX <= 8 || f <= 8) {
+#endif
 #pragma unroll
 				for (int g = 0; g < 4; g++) bsm3_mul(T + 8 * g, W, T + 8 * g);
-			} else if (FMAX <= 16 || f <= 16) {
+			} else if (FMAX <= 16
+#ifndef RD_EXP_K1ONLY
+			           || f <= 16
+#endif
+			           ) {
 #pragma unroll
 				for (int g = 0; g < 2; g++) bsm4_mul(T + 16 * g, W, T + 16 * g);
 			} else {
@@ -409,6 +440,34 @@ __global__ __launch_bounds__(64 * L, 2) void antt_rd_pass(RdParams P, const RdPa
 		// ---- back to compact words, then whole elements straight to HBM
 		transpose32(A);
 		transpose32(B);
+		if (P.outmode == 1) {
+			// EXPERIMENT: stage through the planes, gather 16-byte elements, coalesced stores
+			{
+				char* ypw = lds + y * kPlaneBytes;
+				const uint32_t ba = blk_byte(qa), bb = blk_byte(qb);
+#pragma unroll
+				for (int c = 0; c < 8; c++) {
+					lds_wr4(ypw, ba ^ (16u * c), A + 4 * c);
+					lds_wr4(ypw, bb ^ (16u * c), B + 4 * c);
+				}
+			}
+			__syncthreads();
+#pragma unroll 4
+			for (int r = 0; r < kTileBlocks * 32 / (64 * L); r++) {
+				const int u = tid + 64 * L * r;  // element of the tile
+				const uint32_t q = (uint32_t)(u >> 5), e = (uint32_t)(u & 31);
+				const uint32_t o = (blk_byte(q) ^ (16u * (e >> 2))) + 4u * (e & 3);
+				uint32_t v[4];
+#pragma unroll
+				for (int l = 0; l < L; l++) v[l] = *(const uint32_t*)(lds + l * kPlaneBytes + o);
+				uint32_t* dp = dst + (ooff | tile_off(q)) * L + (size_t)e * L;
+				if (L == 4)
+					st_stream(dp, make_uint4(v[0], v[1], v[2], v[3]));
+				else
+					*dp = v[0];
+			}
+			return;
+		}
 #pragma unroll
 		for (int h = 0; h < 2; h++) {
 			const uint32_t* Z = h ? B : A;
@@ -602,12 +661,18 @@ int rd_prepare(bn_antt_plan* plan) {
 	return BN_OK;
 }
 
+int bs_launch_pass(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st);
+
 // one launch of pass i
 static int rd_launch_one(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* d_out, size_t batch,
                          hipStream_t st) {
 	const rd::RdPass& pass = ((const rd::RdPass*)plan->rd_host.data())[i];
+	static const int hyb = getenv("BN_RD_HYB") ? atoi(getenv("BN_RD_HYB")) : 1;  // EXPERIMENT
+	if (hyb && pass.role == rd::ROLE_LAST) return bs_launch_pass(plan, i, d_in, d_out, batch, st);
 	const rd::RdPass* tab = (const rd::RdPass*)plan->rd_tables + i;
-	rd::RdParams prm{d_in, d_out, plan->log_h, plan->log_rate};
+	static const int outmode = getenv("BN_RD_OUT") ? atoi(getenv("BN_RD_OUT")) : 0;  // EXPERIMENT
+	static const int dbg = getenv("BN_RD_DBG") ? atoi(getenv("BN_RD_DBG")) : 0;  // EXPERIMENT
+	rd::RdParams prm{d_in, d_out, plan->log_h, plan->log_rate, outmode, dbg};
 	const int L = plan->limbs;
 	const size_t ntiles = (batch << plan->log_rate) << pass.n_outer;
 	int rc = timing_begin(plan, i, st);

@@ -427,7 +427,7 @@ extern "C" int bn_bb31_ntt_plan_create(int device, uint32_t generator, int log_g
 	}
 	(void)kR2;
 	int prev = 0;
-	hipGetDevice(&prev);
+	(void)hipGetDevice(&prev);
 	hipError_t e = hipSetDevice(device);
 	if (e == hipSuccess) e = hipMalloc(&P->wtab, tab.size() * sizeof(uint32_t));
 	if (e == hipSuccess) e = hipMemcpy(P->wtab, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
@@ -435,7 +435,7 @@ extern "C" int bn_bb31_ntt_plan_create(int device, uint32_t generator, int log_g
 		for (const void* f : {pass_fn<0>(), pass_fn<1>(), pass_fn<2>(), pass_r_fn(0, 6), pass_r_fn(0, 7), pass_r_fn(0, 8),
 		                      pass_r_fn(0, 9), pass_r_fn(1, 6), pass_r_fn(1, 7), pass_r_fn(1, 8), pass_r_fn(1, 9)})
 			if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, ((1 << kMaxM) * kCols + (1 << 12)) * 4);
-	hipSetDevice(prev);
+	(void)hipSetDevice(prev);
 	if (e != hipSuccess) {
 		bn_bb31_ntt_plan_destroy(P);
 		BN_FAIL(BN_ERR_HIP, "bb31 plan allocation failed: %s", hipGetErrorString(e));
@@ -447,13 +447,13 @@ extern "C" int bn_bb31_ntt_plan_create(int device, uint32_t generator, int log_g
 extern "C" int bn_bb31_ntt_plan_destroy(bn_bb31_ntt_plan* P) {
 	if (!P) return BN_OK;
 	int prev = 0;
-	hipGetDevice(&prev);
-	hipSetDevice(P->device);
-	if (P->wtab) hipFree(P->wtab);
-	if (P->scratch) hipFree(P->scratch);
-	if (P->h_dev) hipFree(P->h_dev);
-	if (P->own_stream) hipStreamDestroy(P->own_stream);
-	hipSetDevice(prev);
+	(void)hipGetDevice(&prev);
+	(void)hipSetDevice(P->device);
+	if (P->wtab) (void)hipFree(P->wtab);
+	if (P->scratch) (void)hipFree(P->scratch);
+	if (P->h_dev) (void)hipFree(P->h_dev);
+	if (P->own_stream) (void)hipStreamDestroy(P->own_stream);
+	(void)hipSetDevice(prev);
 	delete P;
 	return BN_OK;
 }
@@ -513,10 +513,10 @@ extern "C" int bn_bb31_ntt_forward_device(bn_bb31_ntt_plan* P, const uint32_t* d
 	const char* b = (const char*)d_out;
 	BN_CHECK_ARG(a + bytes <= b || b + bytes <= a, "d_in and d_out must not overlap");
 	int prev = 0;
-	hipGetDevice(&prev);
+	(void)hipGetDevice(&prev);
 	if (prev != P->device) BN_HIP(hipSetDevice(P->device));
 	const int rc = bb_forward(P, d_in, d_out, batch, in_bit_reversed, (hipStream_t)stream);
-	if (prev != P->device) hipSetDevice(prev);
+	if (prev != P->device) (void)hipSetDevice(prev);
 	return rc;
 }
 
@@ -529,7 +529,7 @@ extern "C" int bn_bb31_ntt_forward_host(bn_bb31_ntt_plan* P, const uint32_t* in,
 	const size_t n = (size_t)1 << P->log_n;
 	BN_CHECK_ARG(in_elems == n, "input has %zu elements, plan expects 2^%d", in_elems, P->log_n);
 	int prev = 0;
-	hipGetDevice(&prev);
+	(void)hipGetDevice(&prev);
 	BN_HIP(hipSetDevice(P->device));
 	if (!P->h_dev) BN_HIP(hipMalloc(&P->h_dev, 2 * n * sizeof(uint32_t)));
 	if (!P->own_stream) BN_HIP(hipStreamCreateWithFlags(&P->own_stream, hipStreamNonBlocking));
@@ -539,6 +539,6 @@ extern "C" int bn_bb31_ntt_forward_host(bn_bb31_ntt_plan* P, const uint32_t* in,
 		BN_HIP(hipMemcpyAsync(out, P->h_dev + n, n * 4, hipMemcpyDeviceToHost, P->own_stream));
 		BN_HIP(hipStreamSynchronize(P->own_stream));
 	}
-	hipSetDevice(prev);
+	(void)hipSetDevice(prev);
 	return rc;
 }

@@ -33,17 +33,56 @@ def _device_for(dist, group):
     return torch.device("cpu")
 
 
+class WordExchange:
+    """All-gather of a fixed-length uint32 vector over the group, on preallocated buffers: the
+    words are staged into a (pinned, for RCCL) host tensor, copied once to the send buffer,
+    `all_gather_into_tensor` fills a (world x n) receive buffer on the collective's device, and one
+    copy brings it back to host. int32 carries the bits unchanged (no reduction is asked of the
+    backend). RCCL has no XOR reduction, so XOR-reduce = this gather + a local XOR."""
+
+    def __init__(self, n, group=None):
+        import torch
+        import torch.distributed as dist
+        self.n, self.group = n, group
+        self.world = dist.get_world_size(group)
+        self.dev = _device_for(dist, group)
+        pin = self.dev.type == "cuda"
+        self.h_send = torch.empty(n, dtype=torch.int32, pin_memory=pin)
+        self.h_recv = torch.empty(self.world * n, dtype=torch.int32, pin_memory=pin)
+        self.d_send = torch.empty(n, dtype=torch.int32, device=self.dev)
+        self.d_recv = torch.empty(self.world * n, dtype=torch.int32, device=self.dev)
+        self.seconds = 0.0  # wall time spent in exchanges (staging + collective + copy back)
+        self.calls = 0
+
+    def gather(self, words):
+        import time
+        import torch.distributed as dist
+        t0 = time.perf_counter()
+        w = np.ascontiguousarray(words, dtype=np.uint32).reshape(-1)
+        if w.size != self.n:
+            raise ValueError("WordExchange: %d words, built for %d" % (w.size, self.n))
+        self.h_send.numpy()[:] = w.view(np.int32)
+        if self.dev.type == "cuda":
+            self.d_send.copy_(self.h_send, non_blocking=True)
+            dist.all_gather_into_tensor(self.d_recv, self.d_send, group=self.group)
+            self.h_recv.copy_(self.d_recv)  # synchronous: the host needs the words now
+            out = self.h_recv.numpy()
+        else:
+            dist.all_gather_into_tensor(self.d_recv, self.h_send, group=self.group)
+            out = self.d_recv.numpy()
+        res = out.view(np.uint32).reshape(self.world, self.n).copy()
+        self.seconds += time.perf_counter() - t0
+        self.calls += 1
+        return res
+
+    def xor(self, words):
+        return np.bitwise_xor.reduce(self.gather(words), axis=0)
+
+
 def allgather_words(words, group=None):
     """All-gather a uint32 vector (same length on every rank); returns a (world, n) uint32 array."""
-    import torch
-    import torch.distributed as dist
     w = np.ascontiguousarray(words, dtype=np.uint32).reshape(-1)
-    dev = _device_for(dist, group)
-    t = torch.from_numpy(w.astype(np.int64)).to(dev)  # int64: every backend reduces/gathers it
-    world = dist.get_world_size(group)
-    outs = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(outs, t, group=group)
-    return np.stack([o.cpu().numpy().astype(np.uint32) for o in outs])
+    return WordExchange(w.size, group).gather(w)
 
 
 def xor_allreduce_words(words, group=None):
@@ -61,11 +100,16 @@ class ShardedSumcheck:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.replicated = self.world == 1  # after the endgame gather every rank holds everything
+        self._msg = None  # WordExchange for the (d + 2) x 4 message words, built on first use
+        self.exchange_seconds = 0.0  # per-round message exchanges + the endgame gather
+        self.exchange_rounds = 0
 
     def _gather_if_needed(self):
         if not self.replicated and self.prover.needs_gather():
             mine = self.prover.export_shard()
-            allw = allgather_words(mine, self.group)
+            ex = WordExchange(mine.size, self.group)
+            allw = ex.gather(mine)
+            self.exchange_seconds += ex.seconds
             self.prover.import_gathered(allw.reshape(-1), self.world)
             self.replicated = True
 
@@ -75,7 +119,12 @@ class ShardedSumcheck:
         d1 = pts.shape[0]
         flat = np.concatenate([np.asarray(s, np.uint32).reshape(-1), np.asarray(pts, np.uint32).reshape(-1)])
         if not self.replicated:
-            flat = xor_allreduce_words(flat, self.group)
+            if self._msg is None:
+                self._msg = WordExchange(flat.size, self.group)
+            t = self._msg.seconds
+            flat = self._msg.xor(flat)
+            self.exchange_seconds += self._msg.seconds - t
+            self.exchange_rounds += 1
         return flat[:4].copy(), flat[4:].reshape(d1, 4).copy()
 
     def move_to_next_round(self, challenge):

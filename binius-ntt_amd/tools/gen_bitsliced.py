@@ -10,8 +10,7 @@ gate). Differences that matter on CDNA4:
 * XOR chains and AND->XOR pairs are fused into gfx950's 3-input v_bitop3_b32
   (XOR3 = 0x96, (a&b)^c = 0x6a) through __builtin_amdgcn_bitop3_b32 — hipcc does not form
   XOR3 on its own;
-* the multiplier is split into prep(w) (the w-side Karatsuba operand sums, computed once
-  per twiddle and reused across many words) and mulp(x, prep(w)).
+* every multiplier is alias-safe (all inputs are read before any output is written).
 
 Word i of a bitsliced operand holds bit i (tower basis) of 32 independent field elements.
 Output: binius-ntt_amd/csrc/bitsliced_gen.hpp
@@ -70,37 +69,16 @@ def mul_alpha(d, a, h):
     return a1 + vadd(d, a0, mul_alpha(d, a1, h - 1))
 
 
-def presums(d, a, h):
-    """Karatsuba operand leaves (3^h of them) for a level-h bitsliced operand."""
-    if h == 0:
-        return [a[0]]
-    half = 1 << (h - 1)
-    a0, a1 = a[:half], a[half:]
-    return presums(d, a0, h - 1) + presums(d, a1, h - 1) + presums(d, vadd(d, a0, a1), h - 1)
-
-
 def karatsuba(d, a, b, h):
     """Recursive Karatsuba tower product (binary_tower.cuh:35-50), built depth-first so that
-    node creation order == a low-register-pressure evaluation order. `b` may be given as
-    prepared leaves (list of 3^h nodes, flag via tuple ('leaves', list))."""
-    if isinstance(b, tuple):
-        leaves = b[1]
-        if h == 0:
-            return [d.and_(a[0], leaves[0])]
-        n = 3 ** (h - 1)
-        half = 1 << (h - 1)
-        a0, a1 = a[:half], a[half:]
-        z0 = karatsuba(d, a0, ("leaves", leaves[:n]), h - 1)
-        z2 = karatsuba(d, a1, ("leaves", leaves[n:2 * n]), h - 1)
-        z1 = karatsuba(d, vadd(d, a0, a1), ("leaves", leaves[2 * n:]), h - 1)
-    else:
-        if h == 0:
-            return [d.and_(a[0], b[0])]
-        half = 1 << (h - 1)
-        a0, a1, b0, b1 = a[:half], a[half:], b[:half], b[half:]
-        z0 = karatsuba(d, a0, b0, h - 1)
-        z2 = karatsuba(d, a1, b1, h - 1)
-        z1 = karatsuba(d, vadd(d, a0, a1), vadd(d, b0, b1), h - 1)
+    node creation order == a low-register-pressure evaluation order."""
+    if h == 0:
+        return [d.and_(a[0], b[0])]
+    half = 1 << (h - 1)
+    a0, a1, b0, b1 = a[:half], a[half:], b[:half], b[half:]
+    z0 = karatsuba(d, a0, b0, h - 1)
+    z2 = karatsuba(d, a1, b1, h - 1)
+    z1 = karatsuba(d, vadd(d, a0, a1), vadd(d, b0, b1), h - 1)
     lo = vadd(d, z0, z2)
     hi = vadd(d, vadd(d, z1, lo), mul_alpha(d, z2, h - 1))
     return lo + hi
@@ -399,138 +377,12 @@ def count_ops(lines):
     return sum(1 for l in lines if l.startswith("const uint32_t t"))
 
 
-def gen_prep(h):
-    d = DAG()
-    w = [d.inp("w%d" % i) for i in range(1 << h)]
-    leaves = presums(d, w, h)
-    e = make_emitter(d, leaves)
-    body = e.emit({"w%d" % i: "w[%d]" % i for i in range(1 << h)},
-                  [("wl[%d]" % i, leaves[i]) for i in range(len(leaves))])
-    return body
-
-
-def gen_mulp(h, accumulate=False):
-    """out = x * w  (or out ^= x*w when accumulate) given w's prepared leaves."""
-    d = DAG()
-    n = 1 << h
-    x = [d.inp("x%d" % i) for i in range(n)]
-    wl = [d.inp("wl%d" % i) for i in range(3 ** h)]
-    res = karatsuba(d, x, ("leaves", wl), h)
-    imap = {"x%d" % i: "x%d_" % i for i in range(n)}
-    imap.update({"wl%d" % i: "wl[%d]" % i for i in range(3 ** h)})
-    if accumulate:
-        acc = [d.inp("o%d" % i) for i in range(n)]
-        imap.update({"o%d" % i: "o%d_" % i for i in range(n)})
-        res = [d.xor(r, a) for r, a in zip(res, acc)]
-    e = make_emitter(d, res)
-    body = e.emit(imap, [("out[%d]" % i, res[i]) for i in range(n)])
-    pre = ["const uint32_t x%d_ = x[%d];" % (i, i) for i in range(n)]
-    if accumulate:
-        pre += ["const uint32_t o%d_ = out[%d];" % (i, i) for i in range(n)]
-    return pre + body
-
-
-def leaf_combos(h):
-    """The linear combination (set of w bit indices) of every Karatsuba w-leaf, presums order."""
-    d = DAG()
-    w = [d.inp("w%d" % i) for i in range(1 << h)]
-    leaves = presums(d, w, h)
-    memo = {}
-
-    def comb(n):
-        if n in memo:
-            return memo[n]
-        op, args = d.nodes[n]
-        if op == "in":
-            r = frozenset([int(args[0][1:])])
-        else:
-            r = comb(args[0]) ^ comb(args[1])
-        memo[n] = r
-        return r
-    return [comb(n) for n in leaves]
-
-
-def gen_wpack(h):
-    """Packed w-leaves of a per-lane scalar twiddle: wp[] = the 3^h Karatsuba w-side leaf bits of
-    the compact h-level value t (bits 0 .. 2^h - 1), computed with word-parallel shifts/masks, and
-    the (word, bit) of every leaf (presums order). A leaf is then one v_bfe_i32 at its use instead
-    of a live broadcast word: the multiply needs no 32-word W array (register pressure)."""
-    n = 1 << h
-    words = [[frozenset([i]) if i < n else None for i in range(32)]]
-    lines = ["uint32_t v0 = t;"]
-    names = ["v0"]
-    nxt = [1]
-
-    def fresh():
-        v = "v%d" % nxt[0]
-        nxt[0] += 1
-        return v
-    F = n >> 1
-    while F >= 1:
-        mask = 0
-        for pos in range(32):
-            if pos % (2 * F) < F:
-                mask |= 1 << pos
-        sparse = []
-        for wi, v in enumerate(list(words)):
-            sw = [None] * 32
-            any_ = False
-            for pos in range(32):
-                if pos % (2 * F) < F and pos + F < 32:
-                    a, b = v[pos], v[pos + F]
-                    c = (a or frozenset()) ^ (b or frozenset())
-                    sw[pos] = c if c else None
-                    any_ = any_ or bool(c)
-            if any_:
-                nm = fresh()
-                lines.append("uint32_t %s = BN_BITOP3(%s, %s >> %d, 0x%08xu, 0x28);" % (nm, names[wi], names[wi], F, mask))
-                sparse.append((nm, sw))
-        merged = []
-        for i in range(0, len(sparse) - 1, 2):
-            (na, a), (nb, b) = sparse[i], sparse[i + 1]
-            mw = [a[pos] if pos % (2 * F) < F else (b[pos - F]) for pos in range(32)]
-            nm = fresh()
-            lines.append("uint32_t %s = %s | (%s << %d);" % (nm, na, nb, F))
-            merged.append((nm, mw))
-        if len(sparse) % 2:
-            merged.append(sparse[-1])
-        for nm, mw in merged:
-            names.append(nm)
-            words.append(mw)
-        F >>= 1
-    pos_of = {}
-    for wi, v in enumerate(words):
-        for b in range(32):
-            if v[b] is not None and v[b] not in pos_of:
-                pos_of[v[b]] = (wi, b)
-    where = []
-    for c in leaf_combos(h):
-        where.append(pos_of[c])
-    for wi, nm in enumerate(names):
-        lines.append("wp[%d] = %s;" % (wi, nm))
-    return lines, len(names), where
-
-
-def gen_mulpk(h, where):
-    """out = x * w with w given as packed leaves (gen_wpack): each leaf is a bit-field extract."""
-    d = DAG()
-    n = 1 << h
-    x = [d.inp("x%d" % i) for i in range(n)]
-    wl = [d.inp("wl%d" % i) for i in range(3 ** h)]
-    res = karatsuba(d, x, ("leaves", wl), h)
-    imap = {"x%d" % i: "x%d_" % i for i in range(n)}
-    imap.update({"wl%d" % i: "BN_LEAF(wp[%d], %d)" % where[i] for i in range(3 ** h)})
-    e = make_emitter(d, res)
-    body = e.emit(imap, [("out[%d]" % i, res[i]) for i in range(n)])
-    pre = ["const uint32_t x%d_ = x[%d];" % (i, i) for i in range(n)]
-    return pre + body
-
-
 BARRIER_EVERY = int(os.environ.get("BN_GEN_BARRIER_EVERY", "0"))
 
 
-def gen_full(h, accumulate=False):
-    """out = a * b (or out ^= a * b), both bitsliced, alias-safe."""
+def gen_full(h):
+    """out = a * b, both bitsliced, alias-safe (every input word is read before any output word is
+    written)."""
     d = DAG()
     n = 1 << h
     a = [d.inp("a%d" % i) for i in range(n)]
@@ -538,16 +390,10 @@ def gen_full(h, accumulate=False):
     res = karatsuba(d, a, b, h)
     imap = {"a%d" % i: "a%d_" % i for i in range(n)}
     imap.update({"b%d" % i: "b%d_" % i for i in range(n)})
-    if accumulate:
-        acc = [d.inp("o%d" % i) for i in range(n)]
-        imap.update({"o%d" % i: "o%d_" % i for i in range(n)})
-        res = [d.xor(r, q) for r, q in zip(res, acc)]
     e = make_emitter(d, res, low_pressure=h <= 5)
     body = e.emit(imap, [("out[%d]" % i, res[i]) for i in range(n)], BARRIER_EVERY if h <= 5 else 0)
     pre = ["const uint32_t a%d_ = a[%d];" % (i, i) for i in range(n)]
     pre += ["const uint32_t b%d_ = b[%d];" % (i, i) for i in range(n)]
-    if accumulate:
-        pre += ["const uint32_t o%d_ = out[%d];" % (i, i) for i in range(n)]
     return pre + body
 
 
@@ -575,45 +421,16 @@ def main():
              "#define BN_BITOP3(a, b, c, imm) bn_bitop3_host((a), (b), (c), (imm))",
              "#define BN_SCHED_BARRIER()",
              "#endif",
-             "#if defined(__HIP_DEVICE_COMPILE__)",
-             "#define BN_LEAF(word, bit) ((uint32_t)__builtin_amdgcn_sbfe((int)(word), (bit), 1))",
-             "#else",
-             "#define BN_LEAF(word, bit) ((uint32_t)((int32_t)((word) << (31 - (bit))) >> 31))",
-             "#endif",
              "#define BN_XOR3(a, b, c) BN_BITOP3((a), (b), (c), 0x96)",
              "#define BN_ANDXOR(a, b, c) BN_BITOP3((a), (b), (c), 0x6a)",
              "",
              "namespace bn {", ""]
     stats = []
-    for h in (2, 3, 4, 5):
-        pl = gen_prep(h)
-        parts.append("// prep: %d gates" % count_ops(pl))
-        parts.append(fn("void bsm%d_prep(const uint32_t* __restrict__ w, uint32_t* __restrict__ wl)" % h, pl))
-        ml = gen_mulp(h)
-        parts.append("// mulp: %d gates for 32 products" % count_ops(ml))
-        parts.append(fn("void bsm%d_mulp(const uint32_t* x, const uint32_t* __restrict__ wl, uint32_t* out)" % h, ml))
-        al = gen_mulp(h, accumulate=True)
-        parts.append("// mulp_acc (out ^= x*w): %d gates" % count_ops(al))
-        parts.append(fn("void bsm%d_mulp_acc(const uint32_t* x, const uint32_t* __restrict__ wl, uint32_t* out)" % h, al))
-        stats.append((h, count_ops(pl), count_ops(ml), count_ops(al)))
-        if h >= 3:
-            wl_, nw, where = gen_wpack(h)
-            parts.append("// packed w-leaves of a scalar twiddle: %d words, %d ops" % (nw, sum(1 for l in wl_ if l.startswith("uint32_t v") and "= t;" not in l)))
-            parts.append("constexpr int kBsm%dPackWords = %d;" % (h, nw))
-            parts.append(fn("void bsm%d_wpack(uint32_t t, uint32_t* wp)" % h, wl_))
-            kl = gen_mulpk(h, where)
-            parts.append("// mulpk: %d gates + %d leaf extracts for 32 products" % (count_ops(kl), 3 ** h))
-            parts.append(fn("void bsm%d_mulpk(const uint32_t* x, const uint32_t* wp, uint32_t* out)" % h, kl))
     for h in (2, 3, 4, 5, 6, 7):
         fl = gen_full(h)
         parts.append("// full multiply: %d gates for 32 products" % count_ops(fl))
         parts.append(fn("void bsm%d_mul(const uint32_t* a, const uint32_t* b, uint32_t* out)" % h, fl))
         stats.append((h, "full", count_ops(fl)))
-        if 3 <= h < 6:
-            fa = gen_full(h, accumulate=True)
-            parts.append("// full multiply-accumulate (out ^= a*b): %d gates" % count_ops(fa))
-            parts.append(fn("void bsm%d_mul_acc(const uint32_t* a, const uint32_t* b, uint32_t* out)" % h, fa))
-            stats.append((h, "full_acc", count_ops(fa)))
     parts.append("}  // namespace bn")
     with open(OUT, "w") as f:
         f.write("\n".join(parts) + "\n")
