@@ -72,6 +72,15 @@ struct BsParams {
 	BsPass p;
 };
 
+// timing switches and phase traces exist only in the development build (make BN_DEV=1)
+#ifdef BN_DEV
+#define BS_DBG(P) ((P).dbg)
+#define BS_TRACE(P) ((P).trace != nullptr)
+#else
+#define BS_DBG(P) 0
+#define BS_TRACE(P) false
+#endif
+
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // streaming (non-temporal) 16-byte global accesses: every byte is touched once per pass
 __device__ __forceinline__ uint4 ld_stream(const uint32_t* p) {
@@ -136,7 +145,7 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 	uint32_t* plane = lds + l * kPlane;
 	uint32_t* cu_w = lds + L * kPlane + l * kMaxStages;  // this wave's copy of the uniform twiddle parts
 	const size_t n = (size_t)1 << P.log_h;
-	const bool TR = P.trace != nullptr;
+	const bool TR = BS_TRACE(P);
 	unsigned long long tr[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // load, block, in-word, store, tiles, pre, mul, post
 	auto ts = [&]() -> unsigned long long {
 		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -172,12 +181,12 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 				// compact elements: 16-byte loads, 8*L lanes per 32-element block
 				const int u = tid + r * NT;
 				const int q = u / (8 * L), j = u % (8 * L);
-				gbuf[r] = (P.dbg & 1) ? make_uint4(u, j, q, tid) : ld_stream(s + (ooff | tile_off(q)) * L + 4 * j);
+				gbuf[r] = (BS_DBG(P) & 1) ? make_uint4(u, j, q, tid) : ld_stream(s + (ooff | tile_off(q)) * L + 4 * j);
 			} else {
 				// bitsliced: limb l of block q is 128 contiguous bytes, each wave loads its own plane
 				const int u = lane + r * 64;
 				const int q = u >> 3, j = u & 7;
-				gbuf[r] = (P.dbg & 1) ? make_uint4(u, j, q, tid) : ld_stream(s + (ooff | tile_off(q)) * L + 32 * l + 4 * j);
+				gbuf[r] = (BS_DBG(P) & 1) ? make_uint4(u, j, q, tid) : ld_stream(s + (ooff | tile_off(q)) * L + 32 * l + 4 * j);
 			}
 		}
 	};
@@ -214,7 +223,7 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 			tr[5] += t - t_a;
 			t_a = t;
 		}
-		if (P.dbg & 4) {
+		if (BS_DBG(P) & 4) {
 #pragma unroll
 			for (int i = 0; i < 32; i++) Pr[i] = V[i] ^ W[i];
 		} else {
@@ -317,8 +326,8 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 
 		const int jlow = max(LAST ? 5 : 0, ps.stop_j);
 		for (int j = ps.k - 1; j >= jlow; j--) {
-			if (!(P.dbg & 32)) block_stage(j, lane);
-			if (P.dbg & 64)
+			if (!(BS_DBG(P) & 32)) block_stage(j, lane);
+			if (BS_DBG(P) & 64)
 				asm volatile("" ::: "memory");  // experiment: rely on in-order LDS execution only
 			else
 				wave_lds_sync();
@@ -337,7 +346,7 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 			const int qa = lane, qb = qa | (kTileBlocks / 2);
 			uint32_t* pa = plane + qa * kLimbStride;
 			uint32_t* pb = plane + qb * kLimbStride;
-			for (int s = 4; s >= ((P.dbg & 16) ? 5 : ps.stop_j); s--) {  // bottom pass starts at stage 0: j == s
+			for (int s = 4; s >= ((BS_DBG(P) & 16) ? 5 : ps.stop_j); s--) {  // bottom pass starts at stage 0: j == s
 				const int d = 1 << s;
 				const uint32_t um = ~lane_mask(s);  // u-lanes (bit s clear)
 				const uint32_t cb = cu_w[s] ^ tile_tw(s, qb);
@@ -354,7 +363,7 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 				// ca = cb ^ twt[s][6] on A's (um) lanes; the host folds the um & twt[s][6] part into pat
 #pragma unroll
 				for (int i = 0; i < 32; i++) W[i] = ps.pat[s][i] ^ (uint32_t)__builtin_amdgcn_sbfe(cb, i, 1);
-				if (P.dbg & 4) {
+				if (BS_DBG(P) & 4) {
 #pragma unroll
 					for (int i = 0; i < 32; i++) T[i] ^= W[i];
 				} else {
@@ -410,7 +419,7 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 					const int word = 4 * j + t;
 					w[t] = lds[(word % L) * kPlane + q * kLimbStride + word / L];
 				}
-				if (!(P.dbg & 2)) st_stream(dst + (outer_off | tile_off(q)) * L + 4 * j, make_uint4(w[0], w[1], w[2], w[3]));
+				if (!(BS_DBG(P) & 2)) st_stream(dst + (outer_off | tile_off(q)) * L + 4 * j, make_uint4(w[0], w[1], w[2], w[3]));
 			}
 		} else {
 #pragma unroll 4
@@ -418,7 +427,7 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 				const int u = lane + r * 64;
 				const int q = u >> 3, j = u & 7;
 				const uint4 g = *(const uint4*)(plane + q * kLimbStride + 4 * j);
-				if (!(P.dbg & 2)) st_stream(dst + (outer_off | tile_off(q)) * L + 32 * l + 4 * j, g);
+				if (!(BS_DBG(P) & 2)) st_stream(dst + (outer_off | tile_off(q)) * L + 32 * l + 4 * j, g);
 			}
 		}
 		if (TR) {
@@ -718,7 +727,7 @@ struct RtParams {
 		asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");              \
 		ts[k] = __builtin_amdgcn_s_memtime();                                    \
 	}
-#define RT_DBG(f) (P.dbg & (f))
+#define RT_DBG(f) (BS_DBG(P) & (f))
 #else
 #define RT_TS(k)
 #define RT_DBG(f) false

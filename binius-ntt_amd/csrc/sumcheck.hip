@@ -258,7 +258,9 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_messages(ScArgs A) {
 	uint32_t* last = accL + 4 * (kMaxD + 1);  // (a static __shared__ word cost a workgroup per CU)
 	__syncthreads();
 	if (threadIdx.x == 0)
-		*last = __hip_atomic_fetch_add(A.acc + kAccCount, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+		// acq_rel: release orders this workgroup's XORs before its count, acquire makes every other
+		// workgroup's XORs visible to the last one (once per round, so the cost does not matter)
+		*last = __hip_atomic_fetch_add(A.acc + kAccCount, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
 	__syncthreads();
 	if (!*last) return;
 	__threadfence();
@@ -391,6 +393,10 @@ struct bn_sumcheck {
 	// move_to_next_round queues the next round's messages kernel right behind the fold, so the
 	// GPU never waits for the host's next call (composition_eval, which only folds, does not)
 	bool msgs_queued = false, eager = true;
+	// BN_SUMCHECK_FULL_POINTS=1 (read when the prover is created): every round computes p(1) and
+	// the sum from the data instead of deriving them from the claim, so the verifier's
+	// p(0) + p(1) == previous p(r) check also tests the folds (tests/test_gpu_sumcheck.py)
+	bool derive_p1 = !(getenv("BN_SUMCHECK_FULL_POINTS") && atoi(getenv("BN_SUMCHECK_FULL_POINTS")) != 0);
 };
 
 namespace {
@@ -810,8 +816,8 @@ extern "C" int bn_sumcheck_move_to_next_round(bn_sumcheck* sc, const uint32_t* c
 	if (rc != BN_OK) return rc;
 	// no sync: the fold is ordered before the next round's messages on the prover's stream
 	sc->have_claim = false;  // a claim not consumed by this round's messages is stale now
-	sc->claim_pending = sc->have_pts;
-	if (sc->have_pts) memcpy(sc->pending_r, challenge, 16);
+	sc->claim_pending = sc->have_pts && sc->derive_p1;
+	if (sc->claim_pending) memcpy(sc->pending_r, challenge, 16);
 	sc->have_pts = false;
 	sc->cur /= 2;
 	sc->round++;

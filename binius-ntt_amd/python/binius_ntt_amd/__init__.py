@@ -273,8 +273,9 @@ class AdditiveNTT:
         return v.value
 
     def set_variant(self, variant):
-        """0: compact tiles, per-butterfly twiddles; 1: bitsliced LDS tiles; 2: bitsliced register tiles
-        (default for log_h >= 12)."""
+        """0: compact tiles, per-butterfly twiddles (default for log_h < 12); 1: bitsliced LDS tiles
+        (default for log_h >= 12); 2: bitsliced register tiles; 3: round-scheduled bitsliced tiles
+        (log_rate <= 4). Variants 1-3 need log_h >= 12; results are identical."""
         _check(lib().bn_antt_plan_set_variant(self._plan, variant))
 
     def set_event_timing(self, enable):
@@ -500,9 +501,11 @@ class Sumcheck:
                                             ev.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(p)))
         else:
             _check_device_tensor(evals, composition_size * 4 << num_vars, "evals")
-            # the library copies on its own stream: the producer (an NTT, a torch kernel) must be done
-            import torch
-            torch.cuda.current_stream(evals.device).synchronize()
+            # the library copies on its own stream: the producer (an NTT, a torch kernel) must be done.
+            # A raw device address (int) carries no stream: the caller must have synchronised it.
+            if not isinstance(evals, int):
+                import torch
+                torch.cuda.current_stream(evals.device).synchronize()
             _check(lib().bn_sumcheck_create_device(device, num_vars, composition_size,
                                                    1 if data_is_transposed else 0, _ptr(evals), 0, ctypes.byref(p)))
         self._sc = p
@@ -521,11 +524,19 @@ class Sumcheck:
         self._sum_p, self._pts_p, self._ch_p = (b.ctypes.data_as(u32p) for b in (self._sum_buf, self._pts_buf, self._ch_buf))
 
     @classmethod
-    def from_shard(cls, num_vars, composition_size, local_evals, rank, world, device=0, stream=None):
+    def from_shard(cls, num_vars, composition_size, local_evals, rank, world, device=None, stream=None):
         """Shard prover from this rank's share only (bn_sumcheck_create_shard_device): local_evals
         is a device tensor of composition_size * 4 * 2^num_vars / world words (bitsliced batches
-        b with b mod world == rank, in order); the copy is ordered after `stream`."""
+        b with b mod world == rank, in order); the copy is ordered after `stream`. The prover runs
+        on local_evals' device (`device`, if given, must name the same one)."""
         _check_device_tensor(local_evals, composition_size * (4 << num_vars) // world, "local_evals")
+        if not isinstance(local_evals, int):
+            if device is None:
+                device = local_evals.device.index
+            elif device != local_evals.device.index:
+                raise ValueError("device %d does not hold local_evals (cuda:%d)" % (device, local_evals.device.index))
+        elif device is None:
+            device = 0
         self = cls.__new__(cls)
         self.num_vars, self.d = num_vars, composition_size
         p = ctypes.c_void_p()

@@ -80,8 +80,8 @@ int bn_antt_plan_query(const bn_antt_plan* plan, int what, int64_t* value);
  * recomputed per butterfly from the subspace table (the reference kernel's scheme), 1 = bitsliced
  * tiles with host-tabulated twiddle contributions (default when log_h >= 12), 2 = the same
  * passes with register-resident tiles (lane-to-lane exchanges instead of LDS stages; measured
- * slower than 1 except for GF(2^8)-only passes). Variants 1 and 2 need
- * log_h >= 12; results are identical. */
+ * slower than 1 except for GF(2^8)-only passes), 3 = round-scheduled
+ * bitsliced tiles (log_rate <= 4). Variants 1-3 need log_h >= 12; results are identical. */
 int bn_antt_plan_set_variant(bn_antt_plan* plan, int variant);
 
 /* Profiling hook for bench.py: records hipEvents around every kernel launch of the next
@@ -91,8 +91,8 @@ int bn_antt_get_event_timing(bn_antt_plan* plan, float* ms_per_kind, int max_kin
 /* Profiling (no reference counterpart; bench.py's roofline): every pass of the transform is
  * launched `reps` times back to back on `stream` between two hipEvents, giving its steady-state
  * duration per launch in ms_per_pass[pass]. d_out's contents are meaningless afterwards (passes
- * are re-applied to their own output; their cost does not depend on the values). Variant 1
- * only. Synchronous. */
+ * are re-applied to their own output; their cost does not depend on the values). Variants
+ * 1-3. Synchronous. */
 int bn_antt_time_passes(bn_antt_plan* plan, const void* d_in, void* d_out, size_t batch, int reps,
                         void* stream, float* ms_per_pass, int max_passes, int* n_passes);
 

@@ -62,9 +62,14 @@ def test_sumcheck_transcript_quad_path(dev):
     sc.close()
 
 
+@pytest.mark.parametrize("full_points", [False, True])
 @pytest.mark.parametrize("n,d", [(16, 3), (14, 4), (15, 2)])
-def test_sumcheck_protocol_checks(n, d, dev):
-    # the reference test's verifier loop (test.cu:31-100) on a bitsliced input
+def test_sumcheck_protocol_checks(n, d, full_points, dev, monkeypatch):
+    # the reference test's verifier loop (test.cu:31-100) on a bitsliced input. With
+    # BN_SUMCHECK_FULL_POINTS=1 every p(1) and sum comes from the data (no claim-derived point 1),
+    # so p(0) + p(1) == previous p(r) checks the folds as the reference's loop does.
+    if full_points:
+        monkeypatch.setenv("BN_SUMCHECK_FULL_POINTS", "1")
     ev, ch = _case(n, d, 77 + n)
     bs = O.bitslice128(ev)
     sc = B.Sumcheck(n, d, True, bs)
