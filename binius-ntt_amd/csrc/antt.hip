@@ -256,7 +256,7 @@ extern "C" int bn_antt_plan_create(int device, int field_bits, int log_h, int lo
 		// BN_ANTT_VARIANT=1|2|3 overrides the default fast-path kernel for new plans (A/B runs)
 		if (rc == BN_OK && getenv("BN_ANTT_VARIANT")) {
 			const int v = atoi(getenv("BN_ANTT_VARIANT"));
-			if ((v == 1 || v == 2) || (v == 3 && rd_supports(p))) p->variant = v;
+			if ((v == 1 || v == 2 || v == 4) || (v == 3 && rd_supports(p))) p->variant = v;
 		}
 		if (rc != BN_OK) {
 			(void)hipSetDevice(dev_prev);
@@ -369,8 +369,8 @@ extern "C" int bn_antt_plan_query(const bn_antt_plan* p, int what, int64_t* valu
 
 extern "C" int bn_antt_plan_set_variant(bn_antt_plan* p, int variant) {
 	BN_CHECK_ARG(p != nullptr, "plan is NULL");
-	BN_CHECK_ARG(variant >= 0 && variant <= 3, "variant must be 0, 1, 2 or 3");
-	if (variant != 0 && !bs_supports(p)) BN_FAIL(BN_ERR_UNSUPPORTED, "variants 1-3 need log_h >= 12");
+	BN_CHECK_ARG(variant >= 0 && variant <= 4, "variant must be 0, 1, 2, 3 or 4");
+	if (variant != 0 && !bs_supports(p)) BN_FAIL(BN_ERR_UNSUPPORTED, "variants 1-4 need log_h >= 12");
 	if (variant == 3 && !rd_supports(p)) BN_FAIL(BN_ERR_UNSUPPORTED, "variant 3 needs log_rate <= 4");
 	if (variant != 0 && p->variant == 0) {
 		int prev = 0;
@@ -381,7 +381,7 @@ extern "C" int bn_antt_plan_set_variant(bn_antt_plan* p, int variant) {
 		// BN_ANTT_VARIANT=1|2|3 overrides the default fast-path kernel for new plans (A/B runs)
 		if (rc == BN_OK && getenv("BN_ANTT_VARIANT")) {
 			const int v = atoi(getenv("BN_ANTT_VARIANT"));
-			if ((v == 1 || v == 2) || (v == 3 && rd_supports(p))) p->variant = v;
+			if ((v == 1 || v == 2 || v == 4) || (v == 3 && rd_supports(p))) p->variant = v;
 		}
 		(void)hipSetDevice(prev);
 		if (rc != BN_OK) return rc;
@@ -405,7 +405,7 @@ extern "C" int bn_antt_time_passes(bn_antt_plan* p, const void* d_in, void* d_ou
 	BN_CHECK_ARG(p != nullptr && d_in != nullptr && d_out != nullptr && ms_per_pass != nullptr && n_passes != nullptr,
 	             "NULL argument");
 	BN_CHECK_ARG(batch >= 1 && reps >= 1, "batch and reps must be >= 1");
-	if (p->variant == 0) BN_FAIL(BN_ERR_UNSUPPORTED, "pass timing is built for kernel variants 1-3");
+	if (p->variant == 0) BN_FAIL(BN_ERR_UNSUPPORTED, "pass timing is built for kernel variants 1-4");
 	int dev_prev = 0;
 	(void)hipGetDevice(&dev_prev);
 	if (dev_prev != p->device) BN_HIP(hipSetDevice(p->device));

@@ -31,34 +31,10 @@
 #include <cstring>
 #include <vector>
 
-#include "antt_plan.hpp"
+#include "antt_bs.hpp"
 #include "bitsliced.hpp"
 
 namespace bn {
-
-constexpr int kBlkBits = 7;
-constexpr int kTileBlocks = 1 << kBlkBits;
-constexpr int kLimbStride = 36;  // LDS words per (block, limb): 32 + 4 pad (bank spread)
-constexpr int kMinLogH = kBlkBits + 5;
-constexpr int kMaxStages = kBlkBits + 5;  // stages per pass
-constexpr int kMaxOuter = 32 - 5 - kBlkBits;
-constexpr int kMaxRateBits = 8;
-
-enum { ROLE_FIRST = 0, ROLE_MID = 1, ROLE_LAST = 2, ROLE_SINGLE = 3 };
-
-// One pass = k consecutive stages lo..lo+k-1 over every tile. Passed by value as a kernel
-// argument (~2.6 KB), so every table read is a scalar load from the kernarg segment.
-struct BsPass {
-	int lo, k, role, n_outer, stop_j;
-	int bb[kBlkBits];                        // index bit of tile block bit m
-	int ob[kMaxOuter];                       // fixed (outer) index bits, ascending
-	int stage_m[kMaxStages];                 // tile bit of stage lo + j (stages >= 5)
-	int field[kMaxStages];                   // 8/16/32: sub-field holding every twiddle of the stage
-	uint32_t twt[kMaxStages][kBlkBits];      // twiddle contribution of tile block bit m
-	uint32_t two[kMaxStages][kMaxOuter];     // ... of outer bit m
-	uint32_t twc[kMaxStages][kMaxRateBits];  // ... of coset bit c
-	uint32_t pat[5][32];                     // stages 0..4: bit-lane part of the twiddle words
-};
 
 struct BsParams {
 	const uint32_t* src;
@@ -538,7 +514,7 @@ static const void* kernel_for(int L, int role, int fmax, bool pf) {
 	return fmax <= 8 ? kernel_for_f<1, 8>(role, pf) : kernel_for_f<1, 32>(role, pf);
 }
 
-static int pass_fmax(const BsPass& p) {
+int pass_fmax(const BsPass& p) {
 	int f = 8;
 	for (int j = 0; j < p.k; j++) f = std::max(f, p.field[j]);
 	return f;
@@ -561,6 +537,7 @@ int bs_prepare(bn_antt_plan* plan) {
 					BN_HIP(hipFuncSetAttribute(kernel_for(L, role, f, pf != 0), hipFuncAttributeMaxDynamicSharedMemorySize,
 					                           (int)lds_bytes(L)));
 	int rc = rt_prepare();
+	if (rc == BN_OK) rc = rr_prepare(plan);
 	if (rc != BN_OK) return rc;
 	int cus = 0;
 	BN_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, plan->device));
@@ -569,7 +546,7 @@ int bs_prepare(bn_antt_plan* plan) {
 	return BN_OK;
 }
 
-static const BsPass* bs_passes(bn_antt_plan* plan, size_t* n_passes) {
+const BsPass* bs_passes(bn_antt_plan* plan, size_t* n_passes) {
 	// the pass tables depend only on the plan: built once and cached in it
 	if (plan->bs_passes.empty()) {
 		const auto ps = plan_passes(plan);
@@ -610,6 +587,11 @@ static int launch_rt(bn_antt_plan* plan, const BsPass& pass, int i, const uint32
 static int launch_one(bn_antt_plan* plan, const BsPass& pass, int i, const uint32_t* d_in, uint32_t* d_out,
                       size_t batch, hipStream_t st, const BsDevKnobs& kn) {
 	if (plan->variant == 2) return launch_rt(plan, pass, i, d_in, d_out, batch, st, kn);
+	if (plan->variant == 4) {
+		// EXPERIMENT: BN_RR_PASSES = bit mask of the passes that run the register-tile kernel
+		static const int mask = getenv("BN_RR_PASSES") ? (int)strtol(getenv("BN_RR_PASSES"), nullptr, 0) : -1;
+		if ((mask >> i) & 1) return rr_launch_pass(plan, i, d_in, d_out, batch, st);
+	}
 	const int L = plan->limbs;
 	BsParams prm;
 	prm.src = d_in;
@@ -696,21 +678,6 @@ int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t 
 // and store (and the limb interleave of compact data).
 constexpr int kRtPlane = kTileBlocks * kLimbStride + 32;  // words; the +32 staggers planes by half the banks
 constexpr int kRtOutPlane = 4096 + 256;                    // compact out: element e at e + 4*(e >> 6)
-
-struct RtPass {
-	int lo, k, role, n_outer, mlow;
-	int bb[kBlkBits];
-	int ob[kMaxOuter];
-	int jm[kBlkBits];       // stage index (s - lo) of the block stage on tile bit m, -1 if none
-	int field_m[kBlkBits];  // its twiddle sub-field
-	int field_s[5];         // in-word stages s = 0..4 (bottom pass)
-	uint32_t tau[kBlkBits][6];  // block stage on tile bit m: twiddle contribution of lane bit b
-	uint32_t tau_iw[5][6];      // in-word stage s: lane-bit contributions to block R1's twiddle
-	uint32_t cb_const[5];       // in-word stage s: R1's tile-bit-0 contribution
-	uint32_t two[kMaxStages][kMaxOuter];
-	uint32_t twc[kMaxStages][kMaxRateBits];
-	uint32_t pat[5][32];  // in-word stage s: bit-lane part of the twiddle words (R0/R1 difference folded)
-};
 
 struct RtParams {
 	const uint32_t* src;
@@ -1040,7 +1007,7 @@ __global__ __launch_bounds__(64 * L, (RtCfg<ROLE, FMAX>::OCC)) void antt_rt_pass
 // lane bits that lane coordinate c_k depends on
 static const int kCoordDeps[6][2] = {{0, 2}, {1, 2}, {2, -1}, {3, -1}, {4, -1}, {5, -1}};
 
-static int make_rt(const BsPass& p, bool bottom, RtPass* out) {
+int make_rt(const BsPass& p, bool bottom, RtPass* out) {
 	RtPass r;
 	memset(&r, 0, sizeof r);
 	r.lo = p.lo;

@@ -10,8 +10,10 @@
 
 namespace bn {
 
-// In-place 32x32 bit transpose (recursive block swap): afterwards bit j of word i is
-// bit i of word j of the input. Fully unrolled: all indices are compile-time constants.
+// In-place 32x32 bit transpose (recursive block swap): afterwards bit j of word i is bit i of
+// word j of the input. Fully unrolled: all indices are compile-time constants. The 16- and 8-bit
+// levels are byte permutes (one v_perm_b32 per word), the others two selects (v_bitop3) and two
+// shifts per word pair: 256 instructions instead of 400 for the XOR-swap form.
 __device__ __forceinline__ void transpose32(uint32_t* a) {
 #pragma unroll
 	for (int lj = 4; lj >= 0; lj--) {
@@ -24,9 +26,15 @@ __device__ __forceinline__ void transpose32(uint32_t* a) {
 #pragma unroll
 		for (int kk = 0; kk < 16; kk++) {
 			const int k = ((kk & ~(j - 1)) << 1) | (kk & (j - 1));  // the 16 words with bit lj clear
-			const uint32_t t = ((a[k] >> j) ^ a[k + j]) & m;
-			a[k] ^= t << j;
-			a[k + j] ^= t;
+			const uint32_t x = a[k], y = a[k + j];
+			if (lj >= 3) {
+				// v_perm_b32(S0 = y, S1 = x, sel): selector bytes 0-3 pick x's bytes, 4-7 y's
+				a[k] = __builtin_amdgcn_perm(y, x, lj == 4 ? 0x05040100u : 0x06020400u);
+				a[k + j] = __builtin_amdgcn_perm(y, x, lj == 4 ? 0x07060302u : 0x07030501u);
+			} else {
+				a[k] = __builtin_amdgcn_bitop3_b32(m, x, y << j, 0xCA);      // m ? x : y << j
+				a[k + j] = __builtin_amdgcn_bitop3_b32(m, x >> j, y, 0xCA);  // m ? x >> j : y
+			}
 		}
 	}
 }

@@ -150,7 +150,13 @@ class Emitter:
                 continue
             v = "t%d" % cnt[0]
             cnt[0] += 1
-            if op == "and":
+            if op.startswith("csum:"):
+                # compact twiddle combination: bits [0, half) of p ^ (p >> half)
+                lines.append("const uint32_t %s = %s ^ (%s >> %s);" % (v, nm(args[0]), nm(args[0]), op[5:]))
+            elif op.startswith("wleaf:"):
+                # one twiddle bit broadcast to a whole word
+                lines.append("const uint32_t %s = BN_BIT(%s, %s);" % (v, nm(args[0]), op[6:]))
+            elif op == "and":
                 lines.append("const uint32_t %s = %s & %s;" % (v, nm(args[0]), nm(args[1])))
             elif n in fused:
                 x, y = fused[n]
@@ -397,6 +403,174 @@ def gen_full(h):
     return pre + body
 
 
+def kara_w(d, a, cid, off, h):
+    """Karatsuba product of bitsliced a (2^h words) with a twiddle given COMPACTLY: bits
+    [off, off + 2^h) of the per-lane word node cid (the same value in all 32 bit-lanes). The
+    twiddle side never exists as broadcast words: a sub-operand is a bit offset into a compact
+    word (lo, hi halves) or a compact XOR of halves (one shift + XOR), and a leaf is one bit
+    broadcast by v_bfe_i32. Costs ~80 more instructions than the broadcast-word form for GF(2^32)
+    but keeps ~40 fewer registers live."""
+    if h == 0:
+        return [d.and_(a[0], d.node("wleaf:%d" % off, (cid,)))]
+    half = 1 << (h - 1)
+    a0, a1 = a[:half], a[half:]
+    z0 = kara_w(d, a0, cid, off, h - 1)
+    z2 = kara_w(d, a1, cid, off + half, h - 1)
+    if h == 1:
+        wsum = d.xor(d.node("wleaf:%d" % off, (cid,)), d.node("wleaf:%d" % (off + 1), (cid,)))
+        z1 = [d.and_(d.xor(a0[0], a1[0]), wsum)]
+    else:
+        z1 = kara_w(d, vadd(d, a0, a1), d.node("csum:%d" % half, (cid,)), off, h - 1)
+    lo = vadd(d, z0, z2)
+    hi = vadd(d, vadd(d, z1, lo), mul_alpha(d, z2, h - 1))
+    return lo + hi
+
+
+def kara_w_multi(d, aa, cid, off, h):
+    """kara_w for several data operands sharing one compact twiddle, recursing over all of them in
+    lockstep: every twiddle leaf is extracted once and used at once by each operand, so no leaf
+    outlives its uses (the compiler CSEs the leaves of separately inlined products and keeps all
+    of them live)."""
+    if h == 0:
+        leaf = d.node("wleaf:%d" % off, (cid,))
+        return [[d.and_(a[0], leaf)] for a in aa]
+    half = 1 << (h - 1)
+    z0 = kara_w_multi(d, [a[:half] for a in aa], cid, off, h - 1)
+    z2 = kara_w_multi(d, [a[half:] for a in aa], cid, off + half, h - 1)
+    if h == 1:
+        wsum = d.xor(d.node("wleaf:%d" % off, (cid,)), d.node("wleaf:%d" % (off + 1), (cid,)))
+        z1 = [[d.and_(d.xor(a[0], a[1]), wsum)] for a in aa]
+    else:
+        z1 = kara_w_multi(d, [vadd(d, a[:half], a[half:]) for a in aa], d.node("csum:%d" % half, (cid,)), off, h - 1)
+    out = []
+    for k in range(len(aa)):
+        lo = vadd(d, z0[k], z2[k])
+        hi = vadd(d, vadd(d, z1[k], lo), mul_alpha(d, z2[k], h - 1))
+        out.append(lo + hi)
+    return out
+
+
+def gen_fma_tw_multi(h, cnt):
+    """out ^= a * w on cnt consecutive 2^h-word coordinates of a 32-bit limb (a GF(2^(2^h)) twiddle
+    acts on each sub-field coordinate of the tower representation on its own), twiddle leaves
+    shared by the cnt products; eager accumulation at the top level as gen_fma_tw."""
+    d = DAG()
+    n = 1 << h
+    half = n >> 1
+    a = [[d.inp("a%d" % (c * n + i)) for i in range(n)] for c in range(cnt)]
+    w = d.inp("w")
+    o = [[d.inp("o%d" % (c * n + i)) for i in range(n)] for c in range(cnt)]
+    z2 = kara_w_multi(d, [x[half:] for x in a], w, half, h - 1)
+    for c in range(cnt):
+        az2 = mul_alpha(d, z2[c], h - 1)
+        o[c] = [d.xor(o[c][i], z2[c][i]) for i in range(half)] + [d.xor(d.xor(o[c][half + i], z2[c][i]), az2[i]) for i in range(half)]
+    z0 = kara_w_multi(d, [x[:half] for x in a], w, 0, h - 1)
+    for c in range(cnt):
+        o[c] = [d.xor(o[c][i], z0[c][i]) for i in range(half)] + [d.xor(o[c][half + i], z0[c][i]) for i in range(half)]
+    z1 = kara_w_multi(d, [vadd(d, x[:half], x[half:]) for x in a], d.node("csum:%d" % half, (w,)), 0, h - 1)
+    for c in range(cnt):
+        o[c] = o[c][:half] + [d.xor(o[c][half + i], z1[c][i]) for i in range(half)]
+    flat = [x for oc in o for x in oc]
+    imap = {"a%d" % i: "a[%d]" % i for i in range(cnt * n)}
+    imap["w"] = "w"
+    imap.update({"o%d" % i: "out[%d]" % i for i in range(cnt * n)})
+    e = Emitter(d, flat)
+    return e.emit(imap, [("out[%d]" % i, flat[i]) for i in range(cnt * n)], BARRIER_EVERY)
+
+
+def kara_multi(d, aa, b, h):
+    """karatsuba() for several a operands sharing one b, in lockstep (see kara_w_multi)."""
+    if h == 0:
+        return [[d.and_(a[0], b[0])] for a in aa]
+    half = 1 << (h - 1)
+    z0 = kara_multi(d, [a[:half] for a in aa], b[:half], h - 1)
+    z2 = kara_multi(d, [a[half:] for a in aa], b[half:], h - 1)
+    z1 = kara_multi(d, [vadd(d, a[:half], a[half:]) for a in aa], vadd(d, b[:half], b[half:]), h - 1)
+    out = []
+    for k in range(len(aa)):
+        lo = vadd(d, z0[k], z2[k])
+        hi = vadd(d, vadd(d, z1[k], lo), mul_alpha(d, z2[k], h - 1))
+        out.append(lo + hi)
+    return out
+
+
+def gen_acc_multi(h, cnt):
+    """out ^= a * b on cnt consecutive 2^h-word coordinates of a, b (2^h words) shared, in lockstep
+    with eager top-level accumulation (the in-word stages' sub-field twiddle words)."""
+    d = DAG()
+    n = 1 << h
+    half = n >> 1
+    a = [[d.inp("a%d" % (c * n + i)) for i in range(n)] for c in range(cnt)]
+    b = [d.inp("b%d" % i) for i in range(n)]
+    o = [[d.inp("o%d" % (c * n + i)) for i in range(n)] for c in range(cnt)]
+    z2 = kara_multi(d, [x[half:] for x in a], b[half:], h - 1)
+    for c in range(cnt):
+        az2 = mul_alpha(d, z2[c], h - 1)
+        o[c] = [d.xor(o[c][i], z2[c][i]) for i in range(half)] + [d.xor(d.xor(o[c][half + i], z2[c][i]), az2[i]) for i in range(half)]
+    z0 = kara_multi(d, [x[:half] for x in a], b[:half], h - 1)
+    for c in range(cnt):
+        o[c] = [d.xor(o[c][i], z0[c][i]) for i in range(half)] + [d.xor(o[c][half + i], z0[c][i]) for i in range(half)]
+    z1 = kara_multi(d, [vadd(d, x[:half], x[half:]) for x in a], vadd(d, b[:half], b[half:]), h - 1)
+    for c in range(cnt):
+        o[c] = o[c][:half] + [d.xor(o[c][half + i], z1[c][i]) for i in range(half)]
+    flat = [x for oc in o for x in oc]
+    imap = {"a%d" % i: "a[%d]" % i for i in range(cnt * n)}
+    imap.update({"b%d" % i: "b[%d]" % i for i in range(n)})
+    imap.update({"o%d" % i: "out[%d]" % i for i in range(cnt * n)})
+    e = Emitter(d, flat)
+    return e.emit(imap, [("out[%d]" % i, flat[i]) for i in range(cnt * n)], BARRIER_EVERY)
+
+
+def gen_fma_tw(h):
+    """out ^= a * w with w a compact GF(2^(2^h)) value per lane (the same twiddle for the lane's
+    32 bitsliced elements). Top level accumulated eagerly (z2, z0, z1 go into out as soon as each
+    is formed), so at most one half-size partial product is live beside a and out."""
+    d = DAG()
+    n = 1 << h
+    half = n >> 1
+    a = [d.inp("a%d" % i) for i in range(n)]
+    w = d.inp("w")
+    o = [d.inp("o%d" % i) for i in range(n)]
+    a0, a1 = a[:half], a[half:]
+    z2 = kara_w(d, a1, w, half, h - 1)
+    az2 = mul_alpha(d, z2, h - 1)
+    o = [d.xor(o[i], z2[i]) for i in range(half)] + [d.xor(d.xor(o[half + i], z2[i]), az2[i]) for i in range(half)]
+    z0 = kara_w(d, a0, w, 0, h - 1)
+    o = [d.xor(o[i], z0[i]) for i in range(half)] + [d.xor(o[half + i], z0[i]) for i in range(half)]
+    z1 = kara_w(d, vadd(d, a0, a1), d.node("csum:%d" % half, (w,)), 0, h - 1)
+    o = o[:half] + [d.xor(o[half + i], z1[i]) for i in range(half)]
+    imap = {"a%d" % i: "a[%d]" % i for i in range(n)}
+    imap["w"] = "w"
+    imap.update({"o%d" % i: "out[%d]" % i for i in range(n)})
+    e = Emitter(d, o)
+    return e.emit(imap, [("out[%d]" % i, o[i]) for i in range(n)], BARRIER_EVERY)
+
+
+def gen_acc(h):
+    """out ^= a * b (out must not alias a or b): the product's last XOR per word also takes the
+    accumulator, so the register-tile butterflies (u ^= w*v) need no product array."""
+    d = DAG()
+    n = 1 << h
+    half = n >> 1
+    a = [d.inp("a%d" % i) for i in range(n)]
+    b = [d.inp("b%d" % i) for i in range(n)]
+    o = [d.inp("o%d" % i) for i in range(n)]
+    # top level accumulated eagerly (as gen_fma_tw): z2, z0, z1 go into out as soon as formed
+    a0, a1, b0, b1 = a[:half], a[half:], b[:half], b[half:]
+    z2 = karatsuba(d, a1, b1, h - 1)
+    az2 = mul_alpha(d, z2, h - 1)
+    o = [d.xor(o[i], z2[i]) for i in range(half)] + [d.xor(d.xor(o[half + i], z2[i]), az2[i]) for i in range(half)]
+    z0 = karatsuba(d, a0, b0, h - 1)
+    o = [d.xor(o[i], z0[i]) for i in range(half)] + [d.xor(o[half + i], z0[i]) for i in range(half)]
+    z1 = karatsuba(d, vadd(d, a0, a1), vadd(d, b0, b1), h - 1)
+    roots = o[:half] + [d.xor(o[half + i], z1[i]) for i in range(half)]
+    imap = {"a%d" % i: "a[%d]" % i for i in range(n)}
+    imap.update({"b%d" % i: "b[%d]" % i for i in range(n)})
+    imap.update({"o%d" % i: "out[%d]" % i for i in range(n)})
+    e = make_emitter(d, roots, low_pressure=True)
+    return e.emit(imap, [("out[%d]" % i, roots[i]) for i in range(n)], BARRIER_EVERY)
+
+
 def fn(sig, lines):
     # host + device: the device build maps BN_BITOP3 onto v_bitop3_b32, the host build (the
     # reference's __host__ multiply_unrolled<H>, binary_tower_unrolled.cuh:4-5) onto plain logic
@@ -411,7 +585,9 @@ def main():
              "#if defined(__HIP_DEVICE_COMPILE__)",
              "#define BN_BITOP3(a, b, c, imm) __builtin_amdgcn_bitop3_b32((a), (b), (c), (imm))",
              "#define BN_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)",
+             "#define BN_BIT(x, i) ((uint32_t)__builtin_amdgcn_sbfe((int)(x), (i), 1))",
              "#else",
+             "#define BN_BIT(x, i) (0u - (((x) >> (i)) & 1u))",
              "__host__ __device__ constexpr uint32_t bn_bitop3_host(uint32_t a, uint32_t b, uint32_t c, unsigned imm) {",
              "\tuint32_t r = 0;",
              "\tfor (unsigned i = 0; i < 8; i++)",
@@ -431,6 +607,27 @@ def main():
         parts.append("// full multiply: %d gates for 32 products" % count_ops(fl))
         parts.append(fn("void bsm%d_mul(const uint32_t* a, const uint32_t* b, uint32_t* out)" % h, fl))
         stats.append((h, "full", count_ops(fl)))
+        if h in (3, 4, 5):
+            tl = gen_fma_tw(h)
+            parts.append("// out ^= a * w, w compact (bits 0 .. 2^%d - 1 of a per-lane word); out must not alias a: %d gates" % (h, count_ops(tl)))
+            parts.append(fn("void bsm%d_fma_tw(const uint32_t* __restrict__ a, uint32_t w, uint32_t* __restrict__ out)" % h, tl))
+            stats.append((h, "fma_tw", count_ops(tl)))
+            if h < 5:
+                cnt = 32 >> h
+                ml = gen_fma_tw_multi(h, cnt)
+                parts.append("// out ^= a * w on the %d GF(2^%d) coordinates of 32-word limbs, w compact (bits 0 .. 2^%d - 1), twiddle leaves shared: %d gates" % (cnt, 1 << h, h, count_ops(ml)))
+                parts.append(fn("void bsm%dx%d_fma_tw(const uint32_t* __restrict__ a, uint32_t w, uint32_t* __restrict__ out)" % (h, cnt), ml))
+                stats.append((h, "fma_tw x%d" % cnt, count_ops(ml)))
+            if h < 5:
+                cnt = 32 >> h
+                ml = gen_acc_multi(h, cnt)
+                parts.append("// out ^= a * b on the %d GF(2^%d) coordinates of 32-word limbs, b shared (2^%d words): %d gates" % (cnt, 1 << h, h, count_ops(ml)))
+                parts.append(fn("void bsm%dx%d_mul_acc(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint32_t* __restrict__ out)" % (h, cnt), ml))
+                stats.append((h, "acc x%d" % cnt, count_ops(ml)))
+            al = gen_acc(h)
+            parts.append("// out ^= a * b (out must not alias a or b): %d gates" % count_ops(al))
+            parts.append(fn("void bsm%d_mul_acc(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint32_t* __restrict__ out)" % h, al))
+            stats.append((h, "acc", count_ops(al)))
     parts.append("}  // namespace bn")
     with open(OUT, "w") as f:
         f.write("\n".join(parts) + "\n")

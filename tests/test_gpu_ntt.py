@@ -145,31 +145,48 @@ def test_gf128_2p26_limb_md5_and_oracle(ntt_md5, dev):
     assert np.array_equal(y, want)
 
 
-# Kernel variant 2 (register-resident tiles): not the default (measured
-# slower than variant 1), kept parity-green so the A/B numbers in DESIGN.md stay reproducible.
+# Kernel variants 2 (register tiles, LDS exchanges) and 4 (register tiles, three waves per SIMD;
+# DESIGN.md section 5.1): same passes and layouts as variant 1, parity-green so A/B numbers stay
+# reproducible.
+@pytest.mark.parametrize("variant", [2, 4])
 @pytest.mark.parametrize("log_h", [12, 13, 17, 19, 22, 24])
-def test_variant2_gf32_r0_reference_md5(ntt_md5, log_h, dev):
+def test_register_tile_variants_gf32_r0_reference_md5(ntt_md5, log_h, variant, dev):
     x = O.mt_fill(0xDEADBEEF + log_h, 1 << log_h)
     ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(5)))
-    ntt.set_variant(2)
-    assert ntt.variant() == 2
+    ntt.set_variant(variant)
+    assert ntt.variant() == variant
     assert O.md5(_run_device(ntt, x, dev)) == ntt_md5["0"][log_h]
 
 
+@pytest.mark.parametrize("variant", [2, 4])
 @pytest.mark.parametrize("log_h,r", [(12, 3), (13, 0), (14, 4), (17, 2), (20, 0)])
-def test_variant2_gf128_matches_oracle(log_h, r, dev):
+def test_register_tile_variants_gf128_matches_oracle(log_h, r, variant, dev):
     x = O.fill128(0xDEADBEEF + log_h + r, 0x5EED0000, 1 << log_h)
     ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, r, B.FanPaarTowerField(7)))
-    ntt.set_variant(2)
+    ntt.set_variant(variant)
     y = _run_device(ntt, x.reshape(-1), dev).reshape(-1, 4)
     assert np.array_equal(y, O.antt128(x, log_h, r))
 
 
-def test_variant2_gf128_batched(dev):
+@pytest.mark.parametrize("variant", [2, 4])
+def test_register_tile_variants_gf128_batched(variant, dev):
     log_h, batch = 14, 3
     x = O.fill128(0xB00, 0xC0FFEE, batch << log_h)
     ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 1, B.FanPaarTowerField(7)))
-    ntt.set_variant(2)
+    ntt.set_variant(variant)
     y = _run_device(ntt, x.reshape(-1), dev, batch=batch).reshape(batch, -1, 4)
     for b in range(batch):
         assert np.array_equal(y[b], O.antt128(x[b << log_h:(b + 1) << log_h], log_h, 1))
+
+
+def test_variant4_gf128_2p24_limb_md5_and_oracle(ntt_md5, dev):
+    # the north-star size on the register-tile kernel: limb 0 MD5-pinned, all limbs vs the oracle
+    log_h = 24
+    x = O.fill128(0xDEADBEEF + log_h, 0x5EED0000, 1 << log_h)
+    ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(7)))
+    ntt.set_variant(4)
+    y = _run_device(ntt, x.reshape(-1), dev).reshape(-1, 4)
+    assert O.md5_limb(y, 0) == ntt_md5["0"][log_h]
+    want = np.zeros_like(x)
+    O.lib().orc_antt128_limbwise_mt(x.reshape(-1), want.reshape(-1), log_h, 0, O.threads())
+    assert np.array_equal(y, want)
