@@ -133,7 +133,12 @@ def cpu_baseline():
             "sample": "one 2^24-point GF(2^128) additive NTT (r=0) by oracle/antt.c (C port of the reference "
                       "algorithm, butterflies of each stage split over %d pthreads); per_size has 1 thread and "
                       "%d threads at 2^10/2^20/2^24 (%.1f s of CPU work in all)" % (threads, threads, total),
-            "cpu_model": model, "nproc": nproc, "cpus_allowed": allowed, "per_size": per_size}
+            "cpu_model": model, "nproc": nproc, "cpus_allowed": allowed, "per_size": per_size,
+            "share": {"threads_used": threads,
+                      "basis": "OMP_NUM_THREADS=%s: the GPU box's CPU share for one GPU" % os.environ.get("OMP_NUM_THREADS", "unset"),
+                      "full_host_row": "not run: cpus_allowed (%d) is the whole host, which other jobs share; a run "
+                                       "is held to its per-GPU thread share, so the baseline is a %d-thread share of "
+                                       "the host, not the host" % (allowed, threads)}}
 
 
 def limb0_check(d_out, log_h):
@@ -156,25 +161,33 @@ def limb0_check(d_out, log_h):
             "source": "additive_ntt_hashes[0][%d] (src/ulvt/ntt/tests/test_ntt.cu:52-124)" % log_h}
 
 
-def load_pass_counters(log_h):
-    """SQ_INSTS_VALU per launch of each pass from the committed rocprofv3 PMC summary, keyed
-    by log_h and pass index (tools/pmc_summary.py); None if this layout was not profiled."""
-    try:
-        with open(os.path.join(ROOT, "profiles", "r02", "pmc_summary.json")) as f:
-            d = json.load(f)
-        return d.get("log_h=%d" % log_h)
-    except (OSError, ValueError):
-        return None
+PMC_FILE = os.path.join("profiles", "r03", "pmc_kernels.json")
 
 
-def load_traffic(log_h):
-    """HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) per pass."""
+def lib_sha256():
+    import hashlib
+    with open(os.path.join(ROOT, "binius-ntt_amd", "lib", "libbinius_ntt_amd.so"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def kernel_counters(name):
+    """Committed rocprofv3 PMC counters (tools/pmc_summary.py --kernels) of the kernel `name`
+    (demangled; a name without its argument list matches by prefix), or (None, reason) when the
+    profiled library is not this one (SHA-256 of the .so) or the kernel was not profiled."""
     try:
-        with open(os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")) as f:
-            d = json.load(f)
-        return d.get("log_h=%d" % log_h)
+        with open(os.path.join(ROOT, PMC_FILE)) as f:
+            doc = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, "no %s" % PMC_FILE
+    if doc.get("lib_sha256") != lib_sha256():
+        return None, "%s was profiled on another build of the library" % PMC_FILE
+    ks = doc.get("kernels", {})
+    if name in ks:
+        return ks[name], None
+    for k, v in ks.items():
+        if "(" not in name and k.split("(")[0].replace("void ", "") == name:
+            return v, None
+    return None, "kernel %s not in %s" % (name, PMC_FILE)
 
 
 def dry_run(a, json_out):
@@ -313,15 +326,20 @@ def main():
         dom = max(range(len(pass_ms)), key=lambda i: pass_ms[i]) if pass_ms else None
         dom_ms = pass_ms[dom] if dom is not None else ms_step
         achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-        ctr = load_pass_counters(log_h)
-        traffic = load_traffic(log_h)
-        valu = None
-        if ctr and dom is not None and str(dom) in ctr and ctr[str(dom)].get("SQ_INSTS_VALU"):
-            insts = ctr[str(dom)]["SQ_INSTS_VALU"]
+        dom_kernel = ntt.pass_kernel_name(dom) if dom is not None else None
+        ctr, why = kernel_counters(dom_kernel) if dom_kernel else (None, "no pass")
+        traffic = ctr.get("HBM_BYTES") if ctr else None
+        valu = {"kernel": dom_kernel, "insts_per_launch": None, "note": why}
+        if ctr and ctr.get("SQ_INSTS_VALU"):
+            insts = ctr["SQ_INSTS_VALU"]
             rate = insts / (dom_ms * 1e-3)
-            valu = {"insts_per_launch": insts, "achieved": rate, "peak": VALU_PEAK_WAVE_INSTS,
+            valu = {"kernel": dom_kernel, "insts_per_launch": insts, "achieved": rate, "peak": VALU_PEAK_WAVE_INSTS,
                     "unit": "wave64 instructions/s", "frac": rate / VALU_PEAK_WAVE_INSTS,
-                    "source": "profiles/r02/pmc_summary.json"}
+                    # practical ceiling of this instruction mix: independent 3-VGPR-operand v_bitop3_b32
+                    # streams issue at ~0.34 per SIMD-cycle at any occupancy (binius-ntt_amd/tools/
+                    # microbench4.hip), not the nominal 0.5
+                    "bitop3_ceiling_frac": rate / (VALU_PEAK_WAVE_INSTS * 0.34 / 0.5),
+                    "source": PMC_FILE + " (library SHA-256 checked)"}
         res = {
             "metric": "GF(2^128) additive-NTT elements/sec (2^24 pts)",
             "value": elems_per_s,
@@ -347,8 +365,9 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
-                "traffic": traffic.get(str(dom)) if traffic and dom is not None else None,
-                "kernel": "pass %s of %d" % (dom, len(pass_ms)),
+                "traffic": traffic,
+                "traffic_source": (PMC_FILE + ": FETCH_SIZE x 2 + WRITE_SIZE of this kernel") if traffic else why,
+                "kernel": "pass %s of %d: %s" % (dom, len(pass_ms), dom_kernel),
                 "kernel_ms": dom_ms,
                 "pass_ms": pass_ms,
                 "pass_ms_source": "each pass launched back to back between two hipEvents (bn_antt_time_passes)",
@@ -488,27 +507,21 @@ def configs_leg(dev):
     C.c4_phases(dev, lines.append, 24, 3)
     C.c4_phases(dev, lines.append, 28, 3, runs=1)
     # config 2 is VALU-bound (register-resident operands, no HBM traffic): its roofline is the
-    # VALU issue peak, with the kernels' wave-instruction counts per launch from the committed
-    # PMC pass of the same launches (profiles/r02/pmc_c2.json, tools/pmc.sh)
-    pmc = {}
-    try:
-        with open(os.path.join(ROOT, "profiles", "r02", "pmc_c2.json")) as f:
-            pmc = json.load(f)["kernels"]
-    except (OSError, ValueError, KeyError):
-        pass
-    kern = {"compact": "bn::k_repeat_compact", "multiply_unrolled": "bn::k_repeat_bitsliced",
-            "quad-lane": "bn::k_repeat_quad"}
+    # VALU issue peak, with the wave-instruction count per launch of the line's own kernel from the
+    # committed PMC pass (PMC_FILE, matched by kernel name and library hash)
     for ln in lines:
         if "hbm_gbps_algorithmic" in ln:
             ln["hbm_frac_algorithmic"] = ln["hbm_gbps_algorithmic"] / HBM_PEAK_GBPS
-        if ln.get("config") == "c2":
-            k = next((v for key, v in kern.items() if key in ln["workload"]), None)
-            insts = pmc.get(k, {}).get("SQ_INSTS_VALU") if k else None
+        if ln.get("config") == "c2" and ln.get("kernel"):
+            ctr, why = kernel_counters(ln["kernel"])
+            insts = ctr.get("SQ_INSTS_VALU") if ctr else None
             if insts:
                 rate = insts / (ln["ms"] * 1e-3)
-                ln["valu"] = {"kernel": k, "insts_per_launch": insts, "frac": rate / VALU_PEAK_WAVE_INSTS,
+                ln["valu"] = {"kernel": ln["kernel"], "insts_per_launch": insts, "frac": rate / VALU_PEAK_WAVE_INSTS,
                               "lane_insts_per_product": insts * 64 / (ln["value"] * ln["ms"] * 1e-3),
-                              "source": "profiles/r02/pmc_c2.json"}
+                              "source": PMC_FILE + " (library SHA-256 checked)"}
+            else:
+                ln["valu"] = {"kernel": ln["kernel"], "insts_per_launch": None, "note": why}
     return lines
 
 

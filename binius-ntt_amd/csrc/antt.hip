@@ -10,10 +10,13 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <cxxabi.h>
+#include <stdio.h>
+
 #include <algorithm>
 #include <vector>
 
-#include "antt_plan.hpp"
+#include "antt_bs.hpp"
 #include "field_dev.hpp"
 #include "tower.hpp"
 
@@ -256,7 +259,7 @@ extern "C" int bn_antt_plan_create(int device, int field_bits, int log_h, int lo
 		// BN_ANTT_VARIANT=1|2|3 overrides the default fast-path kernel for new plans (A/B runs)
 		if (rc == BN_OK && getenv("BN_ANTT_VARIANT")) {
 			const int v = atoi(getenv("BN_ANTT_VARIANT"));
-			if ((v == 1 || v == 2 || v == 4) || (v == 3 && rd_supports(p))) p->variant = v;
+			if ((v == 1 || v == 2 || v == 4 || v == 5) || (v == 3 && rd_supports(p))) p->variant = v;
 		}
 		if (rc != BN_OK) {
 			(void)hipSetDevice(dev_prev);
@@ -369,8 +372,8 @@ extern "C" int bn_antt_plan_query(const bn_antt_plan* p, int what, int64_t* valu
 
 extern "C" int bn_antt_plan_set_variant(bn_antt_plan* p, int variant) {
 	BN_CHECK_ARG(p != nullptr, "plan is NULL");
-	BN_CHECK_ARG(variant >= 0 && variant <= 4, "variant must be 0, 1, 2, 3 or 4");
-	if (variant != 0 && !bs_supports(p)) BN_FAIL(BN_ERR_UNSUPPORTED, "variants 1-4 need log_h >= 12");
+	BN_CHECK_ARG(variant >= 0 && variant <= 5, "variant must be 0 .. 5");
+	if (variant != 0 && !bs_supports(p)) BN_FAIL(BN_ERR_UNSUPPORTED, "variants 1-5 need log_h >= 12");
 	if (variant == 3 && !rd_supports(p)) BN_FAIL(BN_ERR_UNSUPPORTED, "variant 3 needs log_rate <= 4");
 	if (variant != 0 && p->variant == 0) {
 		int prev = 0;
@@ -381,7 +384,7 @@ extern "C" int bn_antt_plan_set_variant(bn_antt_plan* p, int variant) {
 		// BN_ANTT_VARIANT=1|2|3 overrides the default fast-path kernel for new plans (A/B runs)
 		if (rc == BN_OK && getenv("BN_ANTT_VARIANT")) {
 			const int v = atoi(getenv("BN_ANTT_VARIANT"));
-			if ((v == 1 || v == 2 || v == 4) || (v == 3 && rd_supports(p))) p->variant = v;
+			if ((v == 1 || v == 2 || v == 4 || v == 5) || (v == 3 && rd_supports(p))) p->variant = v;
 		}
 		(void)hipSetDevice(prev);
 		if (rc != BN_OK) return rc;
@@ -405,7 +408,7 @@ extern "C" int bn_antt_time_passes(bn_antt_plan* p, const void* d_in, void* d_ou
 	BN_CHECK_ARG(p != nullptr && d_in != nullptr && d_out != nullptr && ms_per_pass != nullptr && n_passes != nullptr,
 	             "NULL argument");
 	BN_CHECK_ARG(batch >= 1 && reps >= 1, "batch and reps must be >= 1");
-	if (p->variant == 0) BN_FAIL(BN_ERR_UNSUPPORTED, "pass timing is built for kernel variants 1-4");
+	if (p->variant == 0) BN_FAIL(BN_ERR_UNSUPPORTED, "pass timing is built for kernel variants 1-5");
 	int dev_prev = 0;
 	(void)hipGetDevice(&dev_prev);
 	if (dev_prev != p->device) BN_HIP(hipSetDevice(p->device));
@@ -416,6 +419,19 @@ extern "C" int bn_antt_time_passes(bn_antt_plan* p, const void* d_in, void* d_ou
 	                                    ms_per_pass, max_passes, n_passes);
 	if (dev_prev != p->device) (void)hipSetDevice(dev_prev);
 	return rc;
+}
+
+extern "C" int bn_antt_pass_kernel_name(bn_antt_plan* p, int pass, char* buf, size_t cap) {
+	BN_CHECK_ARG(p != nullptr && buf != nullptr && cap > 0, "NULL argument");
+	const void* fn = (p->variant == 1 || p->variant >= 4) ? bs_pass_kernel(p, pass) : nullptr;
+	if (!fn) BN_FAIL(BN_ERR_UNSUPPORTED, "no kernel name for pass %d of variant %d", pass, p->variant);
+	const char* mangled = hipKernelNameRefByPtr(fn, nullptr);
+	if (!mangled) BN_FAIL(BN_ERR_HIP, "hipKernelNameRefByPtr failed");
+	int st = 0;
+	char* dem = abi::__cxa_demangle(mangled, nullptr, nullptr, &st);
+	snprintf(buf, cap, "%s", (st == 0 && dem) ? dem : mangled);
+	free(dem);
+	return BN_OK;
 }
 
 extern "C" int bn_antt_get_event_timing(bn_antt_plan* p, float* ms, int max_kinds, int* n_kinds) {

@@ -542,7 +542,7 @@ int bs_prepare(bn_antt_plan* plan) {
 	int cus = 0;
 	BN_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, plan->device));
 	plan->num_cus = std::max(cus, 1);
-	plan->variant = 1;
+	plan->variant = 5;  // mixed: register tiles for GF(2^8)-only passes, LDS tiles for the others
 	return BN_OK;
 }
 
@@ -587,11 +587,9 @@ static int launch_rt(bn_antt_plan* plan, const BsPass& pass, int i, const uint32
 static int launch_one(bn_antt_plan* plan, const BsPass& pass, int i, const uint32_t* d_in, uint32_t* d_out,
                       size_t batch, hipStream_t st, const BsDevKnobs& kn) {
 	if (plan->variant == 2) return launch_rt(plan, pass, i, d_in, d_out, batch, st, kn);
-	if (plan->variant == 4) {
-		// EXPERIMENT: BN_RR_PASSES = bit mask of the passes that run the register-tile kernel
-		static const int mask = getenv("BN_RR_PASSES") ? (int)strtol(getenv("BN_RR_PASSES"), nullptr, 0) : -1;
-		if ((mask >> i) & 1) return rr_launch_pass(plan, i, d_in, d_out, batch, st);
-	}
+	// variant 4: every pass on register tiles; variant 5 (mixed): register tiles for the passes whose
+	// twiddles all lie in GF(2^8) (their kernel fits four waves per SIMD), LDS tiles for the others
+	if (plan->variant == 4 || (plan->variant == 5 && pass_fmax(pass) <= 8)) return rr_launch_pass(plan, i, d_in, d_out, batch, st);
 	const int L = plan->limbs;
 	BsParams prm;
 	prm.src = d_in;
@@ -647,6 +645,20 @@ int bs_launch_pass(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* d_
 	const int rc = launch_one(plan, passes[i], i, d_in, d_out, batch, st, dev_knobs());
 	plan->variant = saved;
 	return rc;
+}
+
+// the kernel pass i launches under the plan's variant (variants 1, 4, 5), nullptr otherwise
+const void* bs_pass_kernel(bn_antt_plan* plan, int i) {
+	size_t n_passes = 0;
+	const BsPass* passes = bs_passes(plan, &n_passes);
+	if (i < 0 || (size_t)i >= n_passes) return nullptr;
+	const BsPass& pass = passes[i];
+	const int fmax = pass_fmax(pass);
+	if (plan->variant == 4 || (plan->variant == 5 && fmax <= 8)) return rr_pass_kernel(plan, pass);
+	if (plan->variant != 1 && plan->variant != 5) return nullptr;
+	const BsDevKnobs kn = dev_knobs();
+	const bool pf = kn.persist && (kn.pf_mode == 2 || (kn.pf_mode == 1 && fmax <= 8));
+	return kernel_for(plan->limbs, pass.role, fmax, pf);
 }
 
 int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st) {

@@ -61,5 +61,7 @@ int bs_launch_pass(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* d_
 // variant 4 (antt_rr.hip): register-tile kernels over the same passes
 int rr_prepare(bn_antt_plan* plan);
 int rr_launch_pass(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st);
+const void* rr_pass_kernel(bn_antt_plan* plan, const BsPass& pass);
+const void* bs_pass_kernel(bn_antt_plan* plan, int i);
 
 }  // namespace bn

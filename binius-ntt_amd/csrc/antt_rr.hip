@@ -49,7 +49,6 @@ struct RrParams {
 
 constexpr int kSlot = 36;                 // LDS words per staged block (32 + 4 pad: conflict-free b128 writes)
 constexpr int kStagePlane = 64 * kSlot;   // one limb plane of a half tile
-constexpr size_t kStageBytes = 4 * kStagePlane * sizeof(uint32_t);
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void ld4(const uint32_t* p, uint32_t* r) {
@@ -347,6 +346,10 @@ int rr_prepare(bn_antt_plan* plan) {
 				BN_HIP(hipFuncSetAttribute(rr::kernel_for(L, role, f), hipFuncAttributeMaxDynamicSharedMemorySize,
 				                           (int)std::max<size_t>(rr::lds_bytes(L, role), 1)));
 	return BN_OK;
+}
+
+const void* rr_pass_kernel(bn_antt_plan* plan, const BsPass& pass) {
+	return rr::kernel_for(plan->limbs, pass.role, pass_fmax(pass));
 }
 
 // pass i of variant 4 (same pass split and tables as variant 1)

@@ -67,6 +67,7 @@ def lib():
         "bn_antt_set_event_timing": (i32, [vp, i32]),
         "bn_antt_get_event_timing": (i32, [vp, ctypes.POINTER(ctypes.c_float), i32, ctypes.POINTER(i32)]),
         "bn_antt_time_passes": (i32, [vp, vp, vp, sz, i32, vp, ctypes.POINTER(ctypes.c_float), i32, ctypes.POINTER(i32)]),
+        "bn_antt_pass_kernel_name": (i32, [vp, i32, ctypes.c_char_p, sz]),
         "bn_gf128_mul_device": (i32, [vp, vp, vp, sz, vp]),
         "bn_gf128_mul_bitsliced_device": (i32, [vp, vp, vp, sz, vp]),
         "bn_gf32_mul_device": (i32, [vp, vp, vp, sz, vp]),
@@ -273,13 +274,21 @@ class AdditiveNTT:
         return v.value
 
     def set_variant(self, variant):
-        """0: compact tiles, per-butterfly twiddles (default for log_h < 12); 1: bitsliced LDS tiles
-        (default for log_h >= 12); 2: bitsliced register tiles; 3: round-scheduled bitsliced tiles
-        (log_rate <= 4). Variants 1-3 need log_h >= 12; results are identical."""
+        """0: compact tiles, per-butterfly twiddles (default for log_h < 12); 1: bitsliced LDS tiles;
+        2: bitsliced register tiles with LDS exchanges; 3: round-scheduled bitsliced tiles
+        (log_rate <= 4); 4: register tiles (three to four waves per SIMD) on every pass; 5: register
+        tiles for the GF(2^8)-twiddle passes, LDS tiles for the others (default for log_h >= 12).
+        Variants 1-5 need log_h >= 12; results are identical."""
         _check(lib().bn_antt_plan_set_variant(self._plan, variant))
 
     def set_event_timing(self, enable):
         _check(lib().bn_antt_set_event_timing(self._plan, 1 if enable else 0))
+
+    def pass_kernel_name(self, i):
+        """Demangled name of the kernel pass i launches (bn_antt_pass_kernel_name)."""
+        buf = ctypes.create_string_buffer(512)
+        _check(lib().bn_antt_pass_kernel_name(self._plan, i, buf, 512))
+        return buf.value.decode()
 
     def time_passes(self, d_in, d_out, reps=10, batch=1, stream=None):
         """Steady-state ms per launch of each pass (bn_antt_time_passes); d_out is scratch."""

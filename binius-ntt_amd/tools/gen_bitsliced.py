@@ -607,27 +607,28 @@ def main():
         parts.append("// full multiply: %d gates for 32 products" % count_ops(fl))
         parts.append(fn("void bsm%d_mul(const uint32_t* a, const uint32_t* b, uint32_t* out)" % h, fl))
         stats.append((h, "full", count_ops(fl)))
-        if h in (3, 4, 5):
+        # the register-tile NTT kernels (antt_rr.hip) use: the GF(2^32) limb products with a compact
+        # twiddle (h = 5) or with twiddle words (in-word stages), and the sub-field forms on all the
+        # coordinates of a limb at once (h = 3, 4)
+        if h == 5:
             tl = gen_fma_tw(h)
             parts.append("// out ^= a * w, w compact (bits 0 .. 2^%d - 1 of a per-lane word); out must not alias a: %d gates" % (h, count_ops(tl)))
             parts.append(fn("void bsm%d_fma_tw(const uint32_t* __restrict__ a, uint32_t w, uint32_t* __restrict__ out)" % h, tl))
             stats.append((h, "fma_tw", count_ops(tl)))
-            if h < 5:
-                cnt = 32 >> h
-                ml = gen_fma_tw_multi(h, cnt)
-                parts.append("// out ^= a * w on the %d GF(2^%d) coordinates of 32-word limbs, w compact (bits 0 .. 2^%d - 1), twiddle leaves shared: %d gates" % (cnt, 1 << h, h, count_ops(ml)))
-                parts.append(fn("void bsm%dx%d_fma_tw(const uint32_t* __restrict__ a, uint32_t w, uint32_t* __restrict__ out)" % (h, cnt), ml))
-                stats.append((h, "fma_tw x%d" % cnt, count_ops(ml)))
-            if h < 5:
-                cnt = 32 >> h
-                ml = gen_acc_multi(h, cnt)
-                parts.append("// out ^= a * b on the %d GF(2^%d) coordinates of 32-word limbs, b shared (2^%d words): %d gates" % (cnt, 1 << h, h, count_ops(ml)))
-                parts.append(fn("void bsm%dx%d_mul_acc(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint32_t* __restrict__ out)" % (h, cnt), ml))
-                stats.append((h, "acc x%d" % cnt, count_ops(ml)))
             al = gen_acc(h)
             parts.append("// out ^= a * b (out must not alias a or b): %d gates" % count_ops(al))
             parts.append(fn("void bsm%d_mul_acc(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint32_t* __restrict__ out)" % h, al))
             stats.append((h, "acc", count_ops(al)))
+        elif h in (3, 4):
+            cnt = 32 >> h
+            ml = gen_fma_tw_multi(h, cnt)
+            parts.append("// out ^= a * w on the %d GF(2^%d) coordinates of 32-word limbs, w compact (bits 0 .. 2^%d - 1), twiddle leaves shared: %d gates" % (cnt, 1 << h, h, count_ops(ml)))
+            parts.append(fn("void bsm%dx%d_fma_tw(const uint32_t* __restrict__ a, uint32_t w, uint32_t* __restrict__ out)" % (h, cnt), ml))
+            stats.append((h, "fma_tw x%d" % cnt, count_ops(ml)))
+            ml = gen_acc_multi(h, cnt)
+            parts.append("// out ^= a * b on the %d GF(2^%d) coordinates of 32-word limbs, b shared (2^%d words): %d gates" % (cnt, 1 << h, h, count_ops(ml)))
+            parts.append(fn("void bsm%dx%d_mul_acc(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint32_t* __restrict__ out)" % (h, cnt), ml))
+            stats.append((h, "acc x%d" % cnt, count_ops(ml)))
     parts.append("}  // namespace bn")
     with open(OUT, "w") as f:
         f.write("\n".join(parts) + "\n")

@@ -145,10 +145,14 @@ def test_gf128_2p26_limb_md5_and_oracle(ntt_md5, dev):
     assert np.array_equal(y, want)
 
 
-# Kernel variants 2 (register tiles, LDS exchanges) and 4 (register tiles, three waves per SIMD;
-# DESIGN.md section 5.1): same passes and layouts as variant 1, parity-green so A/B numbers stay
-# reproducible.
-@pytest.mark.parametrize("variant", [2, 4])
+# Kernel variants: 1 LDS tiles, 2 register tiles with LDS exchanges, 4
+# register tiles on every pass, 5 (the default for log_h >= 12) register tiles for the GF(2^8)-only
+# passes and LDS tiles for the others. Same passes and layouts; every one parity-green so the A/B
+# numbers stay reproducible.
+VARIANTS = [1, 2, 4, 5]
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("log_h", [12, 13, 17, 19, 22, 24])
 def test_register_tile_variants_gf32_r0_reference_md5(ntt_md5, log_h, variant, dev):
     x = O.mt_fill(0xDEADBEEF + log_h, 1 << log_h)
@@ -158,7 +162,7 @@ def test_register_tile_variants_gf32_r0_reference_md5(ntt_md5, log_h, variant, d
     assert O.md5(_run_device(ntt, x, dev)) == ntt_md5["0"][log_h]
 
 
-@pytest.mark.parametrize("variant", [2, 4])
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("log_h,r", [(12, 3), (13, 0), (14, 4), (17, 2), (20, 0)])
 def test_register_tile_variants_gf128_matches_oracle(log_h, r, variant, dev):
     x = O.fill128(0xDEADBEEF + log_h + r, 0x5EED0000, 1 << log_h)
@@ -168,7 +172,7 @@ def test_register_tile_variants_gf128_matches_oracle(log_h, r, variant, dev):
     assert np.array_equal(y, O.antt128(x, log_h, r))
 
 
-@pytest.mark.parametrize("variant", [2, 4])
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_register_tile_variants_gf128_batched(variant, dev):
     log_h, batch = 14, 3
     x = O.fill128(0xB00, 0xC0FFEE, batch << log_h)
@@ -179,12 +183,14 @@ def test_register_tile_variants_gf128_batched(variant, dev):
         assert np.array_equal(y[b], O.antt128(x[b << log_h:(b + 1) << log_h], log_h, 1))
 
 
-def test_variant4_gf128_2p24_limb_md5_and_oracle(ntt_md5, dev):
-    # the north-star size on the register-tile kernel: limb 0 MD5-pinned, all limbs vs the oracle
+@pytest.mark.parametrize("variant", [1, 4])
+def test_variant_gf128_2p24_limb_md5_and_oracle(ntt_md5, variant, dev):
+    # the north-star size on the non-default kernels (the default is checked by the fixture test
+    # and test_gf128_north_star_size_limb_md5_and_oracle): limb 0 MD5-pinned, all limbs vs the oracle
     log_h = 24
     x = O.fill128(0xDEADBEEF + log_h, 0x5EED0000, 1 << log_h)
     ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, 0, B.FanPaarTowerField(7)))
-    ntt.set_variant(4)
+    ntt.set_variant(variant)
     y = _run_device(ntt, x.reshape(-1), dev).reshape(-1, 4)
     assert O.md5_limb(y, 0) == ntt_md5["0"][log_h]
     want = np.zeros_like(x)

@@ -67,7 +67,8 @@ def c2(dev, out):
         ms = ev_time(lambda: B.gf128_mul_repeat(kind, state, opnd, threads, iters, stream=st), 3, st)
         prods = threads * iters * per
         out({"config": "c2", "workload": "GF(2^128) multiply repeat loop, %s" % name, "value": prods / (ms * 1e-3),
-             "unit": "products/s", "ms": ms, "threads": threads, "iters": iters})
+             "unit": "products/s", "ms": ms, "threads": threads, "iters": iters,
+             "kernel": ("bn::k_repeat_compact", "bn::k_repeat_bitsliced", "bn::k_repeat_quad")[kind]})
     # the boundary entry itself on HBM-resident operands: dst = a * b over 2^20 blocks (32 Mi products;
     # 48 B of HBM traffic per product: two operands read, one product written)
     nblk = 1 << 20
@@ -78,7 +79,7 @@ def c2(dev, out):
     prods = 32 * nblk
     out({"config": "c2", "workload": "GF(2^128) bitsliced products through bn_multiply_unrolled_device(7), 2^20 "
                                      "HBM-resident 128-word blocks", "value": prods / (ms * 1e-3), "unit": "products/s",
-         "ms": ms, "hbm_gbps_algorithmic": 3 * 512.0 * nblk / (ms * 1e-3) / 1e9})
+         "ms": ms, "hbm_gbps_algorithmic": 3 * 512.0 * nblk / (ms * 1e-3) / 1e9, "kernel": "bn::k_gf128_mul_bs"})
     del a, b, o
 
 

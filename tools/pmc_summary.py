@@ -87,7 +87,44 @@ def headline(root, log_h, out_dir):
     print("headline %s: passes %s, traffic %s" % (key, sorted(per_pass), traffic))
 
 
+def lib_sha256():
+    import hashlib
+    path = os.path.join(ROOT, "binius-ntt_amd", "lib", "libbinius_ntt_amd.so")
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def kernels(root, out_path, note):
+    """Per-kernel counters keyed by the exact (demangled) kernel name, stamped with the SHA-256 of
+    the library that was profiled: bench.py uses an entry only when its own library has the same
+    hash and the pass it reports launched exactly that kernel (a kernel change makes it null)."""
+    with open(os.path.join(root, "pmc_summary.json")) as f:
+        summ = json.load(f)
+    ks = {}
+    for k, m in summ.items():
+        e = dict(m)
+        if "HBM_READ_BYTES_corrected" in m and "HBM_WRITE_BYTES" in m:
+            e["HBM_BYTES"] = m["HBM_READ_BYTES_corrected"] + m["HBM_WRITE_BYTES"]
+        ks[k] = e
+    doc = {"lib_sha256": lib_sha256(), "note": note,
+           "units": "per dispatch (mean over the profiled dispatches); FETCH_SIZE/WRITE_SIZE in KiB, "
+                    "HBM_BYTES = 2 x FETCH_SIZE + WRITE_SIZE in bytes (gfx950 correction, MI355X_MICROARCH.md)",
+           "kernels": ks}
+    with open(out_path, "w") as f:
+        json.dump(doc, f, indent=1)
+    print("wrote %s (%d kernels, lib %s)" % (out_path, len(ks), doc["lib_sha256"][:16]))
+
+
 if __name__ == "__main__":
+    # --kernels OUT_PATH NOTE [ROOT]: per-kernel file keyed by exact name + library hash
+    if "--kernels" in sys.argv:
+        i = sys.argv.index("--kernels")
+        out_path, note = sys.argv[i + 1], sys.argv[i + 2]
+        rest = sys.argv[1:i] + sys.argv[i + 3:]
+        sys.argv = [sys.argv[0]] + rest
+        main()
+        kernels(rest[0] if rest else os.path.join(ROOT, "gpurun_out"), out_path, note)
+        sys.exit(0)
     # --headline LOG_H OUT_DIR [ROOT]: summarise ROOT's pmc_* runs, then write the per-pass files
     if "--headline" in sys.argv:
         i = sys.argv.index("--headline")

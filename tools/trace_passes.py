@@ -25,7 +25,7 @@ def main():
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     per = defaultdict(list)
     for r in rows:
-        if "antt_bs_pass" in r["Kernel_Name"] or "antt_rt_pass" in r["Kernel_Name"]:
+        if any(t in r["Kernel_Name"] for t in ("antt_bs_pass", "antt_rt_pass", "antt_rr_pass")):
             per[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     out = {}
     for name, d in sorted(per.items(), key=lambda kv: kv[0]):
