@@ -341,7 +341,7 @@ def main():
                     "bitop3_ceiling_frac": rate / (VALU_PEAK_WAVE_INSTS * 0.34 / 0.5),
                     "source": PMC_FILE + " (library SHA-256 checked)"}
         res = {
-            "metric": "GF(2^128) additive-NTT elements/sec (2^24 pts)",
+            "metric": "GF(2^128) additive-NTT elements/sec (2^%d pts)" % log_h,
             "value": elems_per_s,
             "unit": "elements/s",
             "n_gpus": world,
