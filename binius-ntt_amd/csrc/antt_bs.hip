@@ -482,11 +482,27 @@ static std::vector<BsPass> plan_passes(const bn_antt_plan* plan) {
 	};
 	const int rest = log_h - kMinLogH;
 	const int n_up = (rest + kBlkBits - 1) / kBlkBits;
+	auto gf8_stage = [&](int s) {
+		uint32_t acc = 0;
+		for (int kk = 0; kk < width - s; kk++) acc |= S(s, kk);
+		return acc < 256u;
+	};
 	// upper passes, executed first (highest stages first)
 	int hi = log_h;
 	for (int i = 0; i < n_up; i++) {
 		const int remaining_up = n_up - i;
-		const int k = (hi - kMinLogH + remaining_up - 1) / remaining_up;
+		int k = (hi - kMinLogH + remaining_up - 1) / remaining_up;
+#ifndef BN_UP_EVEN
+		// the first pass takes every top stage whose twiddles lie in GF(2^8) (up to a tile's 7 bits,
+		// as long as the later passes still fit): its register-tile kernel runs near the HBM rate with
+		// VALU to spare, and each stage it takes leaves the GF(2^32) pass one stage less
+		if (i == 0 && remaining_up > 1) {
+			int g = 0;
+			while (g < kBlkBits && hi - g - 1 >= kMinLogH && gf8_stage(hi - g - 1)) g++;
+			const int min_first = (hi - kMinLogH) - (remaining_up - 1) * kBlkBits;  // the rest must still fit
+			if (g > k && g >= min_first) k = g;
+		}
+#endif
 		passes.push_back(make(hi - k, k, false));
 		hi -= k;
 	}
