@@ -323,8 +323,9 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 			uint32_t* pa = plane + qa * kLimbStride;
 			uint32_t* pb = plane + qb * kLimbStride;
 			for (int s = 4; s >= ((BS_DBG(P) & 16) ? 5 : ps.stop_j); s--) {  // bottom pass starts at stage 0: j == s
-				const int d = 1 << s;
-				const uint32_t um = ~lane_mask(s);  // u-lanes (bit s clear)
+				// shift count and lane mask as VGPR operands (an SGPR operand halves the issue rate)
+				const uint32_t d = vgpr(1u << s);
+				const uint32_t um = vgpr(~lane_mask(s));  // u-lanes (bit s clear)
 				const uint32_t cb = cu_w[s] ^ tile_tw(s, qb);
 				uint32_t W[32], T[32];
 #pragma unroll

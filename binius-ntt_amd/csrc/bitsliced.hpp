@@ -10,27 +10,38 @@
 
 namespace bn {
 
+// A uniform value (a constant, a loop-uniform mask or shift count) as a VGPR operand. On gfx950 a
+// VALU instruction that reads an SGPR issues at ~0.21 wave-instructions per SIMD-cycle against
+// ~0.35 for VGPR / inline-constant operands (tools/microbench5.hip), and the compiler puts every
+// non-inline constant and uniform value of these loops into an SGPR: the empty asm ties the value
+// to a VGPR the compiler cannot see through, so it stays there (and is hoisted out of the loops).
+__device__ __forceinline__ uint32_t vgpr(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+	asm("" : "=v"(x) : "0"(x));
+#endif
+	return x;
+}
+
 // In-place 32x32 bit transpose (recursive block swap): afterwards bit j of word i is bit i of
 // word j of the input. Fully unrolled: all indices are compile-time constants. The 16- and 8-bit
 // levels are byte permutes (one v_perm_b32 per word), the others two selects (v_bitop3) and two
 // shifts per word pair: 256 instructions instead of 400 for the XOR-swap form.
 __device__ __forceinline__ void transpose32(uint32_t* a) {
+	// masks and byte selectors as VGPR operands (see vgpr())
+	const uint32_t m2 = vgpr(0x0F0F0F0Fu), m1 = vgpr(0x33333333u), m0 = vgpr(0x55555555u);
+	const uint32_t p4a = vgpr(0x05040100u), p4b = vgpr(0x07060302u), p3a = vgpr(0x06020400u), p3b = vgpr(0x07030501u);
 #pragma unroll
 	for (int lj = 4; lj >= 0; lj--) {
 		const int j = 1 << lj;
-		const uint32_t m = lj == 4 ? 0x0000FFFFu
-						 : lj == 3 ? 0x00FF00FFu
-						 : lj == 2 ? 0x0F0F0F0Fu
-						 : lj == 1 ? 0x33333333u
-								   : 0x55555555u;
+		const uint32_t m = lj == 2 ? m2 : lj == 1 ? m1 : m0;
 #pragma unroll
 		for (int kk = 0; kk < 16; kk++) {
 			const int k = ((kk & ~(j - 1)) << 1) | (kk & (j - 1));  // the 16 words with bit lj clear
 			const uint32_t x = a[k], y = a[k + j];
 			if (lj >= 3) {
 				// v_perm_b32(S0 = y, S1 = x, sel): selector bytes 0-3 pick x's bytes, 4-7 y's
-				a[k] = __builtin_amdgcn_perm(y, x, lj == 4 ? 0x05040100u : 0x06020400u);
-				a[k + j] = __builtin_amdgcn_perm(y, x, lj == 4 ? 0x07060302u : 0x07030501u);
+				a[k] = __builtin_amdgcn_perm(y, x, lj == 4 ? p4a : p3a);
+				a[k + j] = __builtin_amdgcn_perm(y, x, lj == 4 ? p4b : p3b);
 			} else {
 				a[k] = __builtin_amdgcn_bitop3_b32(m, x, y << j, 0xCA);      // m ? x : y << j
 				a[k + j] = __builtin_amdgcn_bitop3_b32(m, x >> j, y, 0xCA);  // m ? x >> j : y
