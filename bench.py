@@ -388,6 +388,11 @@ def main():
         mine = hi - lo
         nb = 1 << a.c5_log_n
         bt_in = torch.randint(-2**31, 2**31 - 1, (max(mine, 1) * 4 * nb,), dtype=torch.int32, device=dev)
+        # limb 0 of this rank's first transform = the reference stream std::mt19937(0xdeadbeef + log_n):
+        # its output limb-0 plane must hash to additive_ntt_hashes[0][log_n] (checked after timing)
+        mt = np.random.RandomState(0xDEADBEEF + a.c5_log_n).randint(0, 2**32, size=nb, dtype=np.uint64).astype(np.uint32)
+        bt_in.view(-1, 4)[:nb, 0] = torch.from_numpy(mt.view(np.int32)).to(dev)
+        del mt
         bt_out = torch.empty_like(bt_in)
         bplan = B.AdditiveNTT(B.AdditiveNTTConf(a.c5_log_n, 0, B.FanPaarTowerField(7), device=local))
         if a.variant is not None:
@@ -400,12 +405,14 @@ def main():
         run_batch()
         torch.cuda.synchronize(dev)
         dtb = timed(run_batch, a.c5_steps) / a.c5_steps
+        c5_check = limb0_check(bt_out[:4 * nb], a.c5_log_n) if mine else None
         c5["batched_ntt"] = {
             "workload": "%d x 2^%d-point GF(2^128) additive NTT, %d per rank (rank-contiguous slices, no collective)"
                         % (a.c5_batch, a.c5_log_n, -(-a.c5_batch // world)),
             "ms": dtb * 1e3, "elements_per_s": a.c5_batch * nb / dtb,
             "per_gpu_hbm_frac": (-(-a.c5_batch // world)) * 32 * nb / dtb / 1e9 / HBM_PEAK_GBPS,
-            "scaling": "strong", "steps": a.c5_steps}
+            "scaling": "strong", "steps": a.c5_steps,
+            "output_check": dict(c5_check, transform="this rank's first") if c5_check else None}
         del bt_in, bt_out, bplan
         torch.cuda.empty_cache()
 
