@@ -49,37 +49,25 @@ __global__ __launch_bounds__(256) void k_bitslice(uint32_t* buf, size_t nblk, in
 // Bitsliced GF(2^128) products o = a * b, 32 per 128-word block (multiply_unrolled<7>,
 // circuit_generator/unrolled/binary_tower_unrolled7.cu:6), on the quad-lane product of
 // quad_mul.hpp: block b runs on the 4 lanes of one quad (lane l loads limb l of both operands into
-// the quad's LDS slot and stores limb l of the product), so no lane holds more than ~4 x 32 words
-// and the kernel runs at 2 waves/SIMD without spills. Every operand word is read into the slot
-// before any output word is written: alias-safe for o == a or o == b (core.cu:21).
+// the quad's LDS slot and stores limb l of the product), so no lane holds more than ~4 x 32 words.
+// One block per quad and no loop: a persistent grid that prefetched the next block's operands
+// kept them live across the product, and the spills (432 B/lane) made it 1.9x slower (3.4e10 vs
+// 6.2-6.5e10 products/s). Every operand word is read into the slot before any
+// output word is written: alias-safe for o == a or o == b (core.cu:21).
 __global__ __launch_bounds__(256, 2) void k_gf128_mul_bs(const uint32_t* a, const uint32_t* b, uint32_t* o, size_t nblk) {
 	extern __shared__ uint32_t lds[];
 	const int l = threadIdx.x & 3, qw = threadIdx.x >> 2;
 	const quad::Slot S{lds + qw * quad::kQuadWords};
-	const size_t step = (size_t)gridDim.x * 64;
-	size_t blk = (size_t)blockIdx.x * 64 + qw;  // uniform per quad
-	if (blk >= nblk) return;                    // whole quads leave together
-	uint32_t pa[32], pb[32];
-	quad::ld32(pa, a + 128 * blk + 32 * l);
-	quad::ld32(pb, b + 128 * blk + 32 * l);
-	for (;;) {
-		quad::wsync();
-		quad::sst(S, l, pa);
-		quad::sst(S, 4 + l, pb);
-		// the next block's operands are in flight during this block's product (registers: the
-		// product parks its operands in the slot, so 64 VGPRs of prefetch fit at 2 waves/SIMD)
-		const size_t nxt = blk + step;
-		if (nxt < nblk) {
-			quad::ld32(pa, a + 128 * nxt + 32 * l);
-			quad::ld32(pb, b + 128 * nxt + 32 * l);
-		}
-		quad::quad_mul<false>(S, nullptr, l);  // row l <- (rows 0..3) * (rows 4..7)
-		uint32_t x[32];
-		quad::sld(x, S, l);
-		quad::st32(o + 128 * blk + 32 * l, x);
-		if (nxt >= nblk) break;
-		blk = nxt;
-	}
+	const size_t blk = (size_t)blockIdx.x * 64 + qw;  // uniform per quad
+	if (blk >= nblk) return;                          // whole quads leave together
+	uint32_t x[32];
+	quad::ld32(x, a + 128 * blk + 32 * l);
+	quad::sst(S, l, x);
+	quad::ld32(x, b + 128 * blk + 32 * l);
+	quad::sst(S, 4 + l, x);
+	quad::quad_mul<false>(S, nullptr, l);  // row l <- (rows 0..3) * (rows 4..7)
+	quad::sld(x, S, l);
+	quad::st32(o + 128 * blk + 32 * l, x);
 }
 static size_t quad_lds_bytes();
 
@@ -182,13 +170,9 @@ int gf128_mul_bitsliced_launch(const void* a, const void* b, void* o, size_t nbl
 	if (!nblk) return BN_OK;
 	int rc = quad_kernel_attr((const void*)k_gf128_mul_bs);
 	if (rc != BN_OK) return rc;
-	int dev = 0, cus = 0;
-	BN_HIP(hipGetDevice(&dev));
-	BN_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-	// 64 blocks per work-group, two work-groups per CU resident: a persistent grid (each quad walks
-	// its blocks with the next block's operands prefetched)
-	size_t grid = (nblk + 63) / 64;
-	grid = std::min(grid, (size_t)std::max(cus, 1) * 2);
+	// 64 blocks per work-group, one per quad
+	const size_t grid = (nblk + 63) / 64;
+	BN_CHECK_ARG(grid <= 0x7fffffffu, "too many blocks for one launch");
 	hipLaunchKernelGGL(k_gf128_mul_bs, dim3((unsigned)grid), dim3(256), quad_lds_bytes(), st, (const uint32_t*)a,
 	                   (const uint32_t*)b, (uint32_t*)o, nblk);
 	BN_HIP(hipGetLastError());

@@ -22,13 +22,19 @@ __device__ __forceinline__ void wsync() {
 	__builtin_amdgcn_wave_barrier();
 }
 
+// 16-byte accesses, register arrays filled and drained component-wise: a uint4 store through a
+// pointer into a register array takes the array's address, and in some kernels SROA then leaves the
+// array in scratch (k_gf128_mul_bs had 272-448 B of private memory per lane from this alone)
 __device__ __forceinline__ void ld32(uint32_t* r, const uint32_t* p) {
 #pragma unroll
-	for (int i = 0; i < 32; i += 4) *(uint4*)(r + i) = *(const uint4*)(p + i);
+	for (int i = 0; i < 32; i += 4) {
+		const uint4 v = *(const uint4*)(p + i);
+		r[i] = v.x, r[i + 1] = v.y, r[i + 2] = v.z, r[i + 3] = v.w;
+	}
 }
 __device__ __forceinline__ void st32(uint32_t* p, const uint32_t* r) {
 #pragma unroll
-	for (int i = 0; i < 32; i += 4) *(uint4*)(p + i) = *(const uint4*)(r + i);
+	for (int i = 0; i < 32; i += 4) *(uint4*)(p + i) = make_uint4(r[i], r[i + 1], r[i + 2], r[i + 3]);
 }
 
 // bitsliced multiply_alpha on GF(2^(2^H)) (binary_tower.cuh multiply_alpha): out may not alias a
