@@ -132,8 +132,8 @@ extern "C" int bn_multiply_unrolled_device(int height, const void* a, const void
 	// <7> (GF(2^128), the sumcheck's product) runs on the quad-lane product, like
 	// bn_gf128_mul_bitsliced_device: one lane per 128-word block spills the 9712-gate circuit
 	if (height == 7) return gf128_mul_bitsliced_launch(a, b, dst, nblocks, (hipStream_t)stream);
-	const void* fns[6] = {(const void*)k_unrolled<2>, (const void*)k_unrolled<3>, (const void*)k_unrolled<4>,
-	                      (const void*)k_unrolled<5>, (const void*)k_unrolled<6>, (const void*)k_unrolled<7>};
+	const void* fns[5] = {(const void*)k_unrolled<2>, (const void*)k_unrolled<3>, (const void*)k_unrolled<4>,
+	                      (const void*)k_unrolled<5>, (const void*)k_unrolled<6>};
 	void* args[] = {&a, &b, &dst, &nblocks};
 	BN_HIP(hipLaunchKernel(fns[height - 2], dim3(grid_for(nblocks)), dim3(256), args, 0, (hipStream_t)stream));
 	return BN_OK;
