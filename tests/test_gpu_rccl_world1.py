@@ -1,0 +1,49 @@
+"""RCCL rehearsal on one GPU: the exact process-group call bench.py makes for N > 1
+(`init_process_group("nccl", device_id=cuda:local)`), the device branch of
+`distributed.WordExchange` (pinned host staging, `all_gather_into_tensor` on the GPU, one copy
+back), the max-over-ranks `all_reduce` and a barrier, all over the nccl (= RCCL) backend with world
+size 1. A single GPU cannot hold two RCCL ranks, so this is as far as the multi-GPU data path can
+run before the driver's 8-GPU bench; its multi-rank logic is covered by the gloo tests
+(tests/test_distributed.py, tests/test_bench_cli.py)."""
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SCRIPT = textwrap.dedent("""
+    import os, sys
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(sys.argv[1], "binius-ntt_amd", "python"))
+    from binius_ntt_amd import distributed as D
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+    ex = D.WordExchange(24)
+    assert ex.dev.type == "cuda"
+    words = np.random.default_rng(7).integers(0, 2**32, size=24, dtype=np.uint64).astype(np.uint32)
+    for _ in range(3):
+        got = ex.gather(words)
+        assert got.shape == (1, 24) and np.array_equal(got[0], words)
+        assert np.array_equal(ex.xor(words), words)
+    t = torch.tensor([1.5], device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.barrier()
+    assert t.item() == 1.5 and ex.calls == 6
+    dist.destroy_process_group()
+    print("rccl world1 ok")
+""")
+
+
+@pytest.mark.gpu
+def test_rccl_process_group_and_word_exchange_world1():
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29533", RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "-c", SCRIPT, ROOT], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "rccl world1 ok" in r.stdout
