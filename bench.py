@@ -121,18 +121,21 @@ def cpu_baseline():
         row = {}
         for nt in (1, threads):
             reps = max(1, min(200, (1 << 20) // (1 << log_h)))
+            used = L.orc_antt_mt_threads(log_h, nt)  # at most one thread per 4096 butterflies of a stage
             t0 = time.perf_counter()
             for _ in range(reps):
                 L.orc_antt128_limbwise_mt(x.reshape(-1), out.reshape(-1), log_h, 0, nt)
             dt = (time.perf_counter() - t0) / reps
             total += dt * reps
-            row["threads_%d" % nt] = {"elements_per_s": (1 << log_h) / dt, "ms": dt * 1e3, "reps": reps}
+            row["threads_%d" % nt] = {"elements_per_s": (1 << log_h) / dt, "ms": dt * 1e3, "reps": reps,
+                                      "threads_used": used}
         per_size["2^%d" % log_h] = row
     head = per_size["2^24"]["threads_%d" % threads]
     return {"value": head["elements_per_s"], "unit": "elements/s", "cores": threads, "kind": "port",
             "sample": "one 2^24-point GF(2^128) additive NTT (r=0) by oracle/antt.c (C port of the reference "
-                      "algorithm, butterflies of each stage split over %d pthreads); per_size has 1 thread and "
-                      "%d threads at 2^10/2^20/2^24 (%.1f s of CPU work in all)" % (threads, threads, total),
+                      "algorithm, butterflies of each stage split over a persistent pool of %d threads); per_size has "
+                      "1 thread and %d threads at 2^10/2^20/2^24, each row with the threads it used (at most "
+                      "one per 4096 butterflies of a stage: 1 at 2^10) (%.1f s of CPU work in all)" % (threads, threads, total),
             "cpu_model": model, "nproc": nproc, "cpus_allowed": allowed, "per_size": per_size,
             "share": {"threads_used": threads,
                       "basis": "OMP_NUM_THREADS=%s: the GPU box's CPU share for one GPU" % os.environ.get("OMP_NUM_THREADS", "unset"),

@@ -204,18 +204,29 @@ int launch_v0(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, hipStre
 	return BN_OK;
 }
 
-// Bitsliced fast path (antt_bs.hip), used when bs_supports(plan).
+// Bitsliced fast path (antt_bs.hip, antt_rr.hip), used when bs_supports(plan).
 int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st);
 bool bs_supports(const bn_antt_plan* plan);
 int bs_prepare(bn_antt_plan* plan);
 int bs_time_passes(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, int reps,
                    hipStream_t st, float* ms, int max_passes, int* n_out);
-// Round-scheduled fast path (antt_rd.hip, variant 3): the default when rd_supports(plan).
-bool rd_supports(const bn_antt_plan* plan);
-int rd_prepare(bn_antt_plan* plan);
-int launch_rd(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st);
-int rd_time_passes(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, int reps, hipStream_t st,
-                   float* ms, int max_passes, int* n_out);
+
+// Kernel variants: 0 compact tiles (log_h < 12), 1 bitsliced LDS tiles (antt_bs_pass), 4 bitsliced
+// register tiles (antt_rr_pass), 5 = 4 for the passes whose twiddles all lie in GF(2^8) and 1 for
+// the others (the default for log_h >= 12).
+static bool valid_variant(int v) { return v == 0 || v == 1 || v == 4 || v == 5; }
+
+// development build only (make BN_DEV=1): BN_ANTT_VARIANT overrides the default kernel of new plans
+static void dev_variant_override(bn_antt_plan* p) {
+#ifdef BN_DEV
+	if (const char* e = getenv("BN_ANTT_VARIANT")) {
+		const int v = atoi(e);
+		if (v != 0 && valid_variant(v)) p->variant = v;
+	}
+#else
+	(void)p;
+#endif
+}
 
 }  // namespace bn
 
@@ -255,12 +266,7 @@ extern "C" int bn_antt_plan_create(int device, int field_bits, int log_h, int lo
 	p->variant = 0;
 	if (bs_supports(p)) {
 		int rc = bs_prepare(p);
-		if (rc == BN_OK && rd_supports(p)) rc = rd_prepare(p);
-		// BN_ANTT_VARIANT=1|2|3 overrides the default fast-path kernel for new plans (A/B runs)
-		if (rc == BN_OK && getenv("BN_ANTT_VARIANT")) {
-			const int v = atoi(getenv("BN_ANTT_VARIANT"));
-			if ((v == 1 || v == 2 || v == 4 || v == 5) || (v == 3 && rd_supports(p))) p->variant = v;
-		}
+		if (rc == BN_OK) dev_variant_override(p);
 		if (rc != BN_OK) {
 			(void)hipSetDevice(dev_prev);
 			bn_antt_plan_destroy(p);
@@ -278,7 +284,6 @@ extern "C" int bn_antt_plan_destroy(bn_antt_plan* p) {
 	(void)hipGetDevice(&dev_prev);
 	(void)hipSetDevice(p->device);
 	if (p->s_dev) (void)hipFree(p->s_dev);
-	if (p->rd_tables) (void)hipFree(p->rd_tables);
 	if (p->scratch) (void)hipFree(p->scratch);
 	if (p->h_dev_in) (void)hipFree(p->h_dev_in);
 	if (p->h_dev_out) (void)hipFree(p->h_dev_out);
@@ -297,7 +302,6 @@ extern "C" int bn_antt_plan_destroy(bn_antt_plan* p) {
 static int forward_device_impl(bn_antt_plan* p, const void* d_in, void* d_out, size_t batch, hipStream_t st) {
 	const size_t n_in = ((size_t)1 << p->log_h) * p->limbs;
 	const size_t n_out = n_in << p->log_rate;
-	if (p->variant == 3) return launch_rd(p, (const uint32_t*)d_in, (uint32_t*)d_out, batch, st);
 	if (p->variant != 0) return launch_bs(p, (const uint32_t*)d_in, (uint32_t*)d_out, batch, st);
 	for (size_t b = 0; b < batch; b++) {
 		int rc = launch_v0(p, (const uint32_t*)d_in + b * n_in, (uint32_t*)d_out + b * n_out, st);
@@ -372,20 +376,13 @@ extern "C" int bn_antt_plan_query(const bn_antt_plan* p, int what, int64_t* valu
 
 extern "C" int bn_antt_plan_set_variant(bn_antt_plan* p, int variant) {
 	BN_CHECK_ARG(p != nullptr, "plan is NULL");
-	BN_CHECK_ARG(variant >= 0 && variant <= 5, "variant must be 0 .. 5");
-	if (variant != 0 && !bs_supports(p)) BN_FAIL(BN_ERR_UNSUPPORTED, "variants 1-5 need log_h >= 12");
-	if (variant == 3 && !rd_supports(p)) BN_FAIL(BN_ERR_UNSUPPORTED, "variant 3 needs log_rate <= 4");
+	BN_CHECK_ARG(valid_variant(variant), "variant must be 0, 1, 4 or 5 (got %d)", variant);
+	if (variant != 0 && !bs_supports(p)) BN_FAIL(BN_ERR_UNSUPPORTED, "variants 1, 4 and 5 need log_h >= 12");
 	if (variant != 0 && p->variant == 0) {
 		int prev = 0;
 		(void)hipGetDevice(&prev);
 		BN_HIP(hipSetDevice(p->device));
-		int rc = bs_prepare(p);
-		if (rc == BN_OK && rd_supports(p)) rc = rd_prepare(p);
-		// BN_ANTT_VARIANT=1|2|3 overrides the default fast-path kernel for new plans (A/B runs)
-		if (rc == BN_OK && getenv("BN_ANTT_VARIANT")) {
-			const int v = atoi(getenv("BN_ANTT_VARIANT"));
-			if ((v == 1 || v == 2 || v == 4 || v == 5) || (v == 3 && rd_supports(p))) p->variant = v;
-		}
+		const int rc = bs_prepare(p);
 		(void)hipSetDevice(prev);
 		if (rc != BN_OK) return rc;
 	}
@@ -408,22 +405,19 @@ extern "C" int bn_antt_time_passes(bn_antt_plan* p, const void* d_in, void* d_ou
 	BN_CHECK_ARG(p != nullptr && d_in != nullptr && d_out != nullptr && ms_per_pass != nullptr && n_passes != nullptr,
 	             "NULL argument");
 	BN_CHECK_ARG(batch >= 1 && reps >= 1, "batch and reps must be >= 1");
-	if (p->variant == 0) BN_FAIL(BN_ERR_UNSUPPORTED, "pass timing is built for kernel variants 1-5");
+	if (p->variant == 0) BN_FAIL(BN_ERR_UNSUPPORTED, "pass timing is built for kernel variants 1, 4 and 5");
 	int dev_prev = 0;
 	(void)hipGetDevice(&dev_prev);
 	if (dev_prev != p->device) BN_HIP(hipSetDevice(p->device));
-	const int rc = p->variant == 3
-	                   ? rd_time_passes(p, (const uint32_t*)d_in, (uint32_t*)d_out, batch, reps, (hipStream_t)stream,
-	                                    ms_per_pass, max_passes, n_passes)
-	                   : bs_time_passes(p, (const uint32_t*)d_in, (uint32_t*)d_out, batch, reps, (hipStream_t)stream,
-	                                    ms_per_pass, max_passes, n_passes);
+	const int rc = bs_time_passes(p, (const uint32_t*)d_in, (uint32_t*)d_out, batch, reps, (hipStream_t)stream,
+	                              ms_per_pass, max_passes, n_passes);
 	if (dev_prev != p->device) (void)hipSetDevice(dev_prev);
 	return rc;
 }
 
 extern "C" int bn_antt_pass_kernel_name(bn_antt_plan* p, int pass, char* buf, size_t cap) {
 	BN_CHECK_ARG(p != nullptr && buf != nullptr && cap > 0, "NULL argument");
-	const void* fn = (p->variant == 1 || p->variant >= 4) ? bs_pass_kernel(p, pass) : nullptr;
+	const void* fn = p->variant != 0 ? bs_pass_kernel(p, pass) : nullptr;
 	if (!fn) BN_FAIL(BN_ERR_UNSUPPORTED, "no kernel name for pass %d of variant %d", pass, p->variant);
 	const char* mangled = hipKernelNameRefByPtr(fn, nullptr);
 	if (!mangled) BN_FAIL(BN_ERR_HIP, "hipKernelNameRefByPtr failed");

@@ -517,15 +517,23 @@ static std::vector<BsPass> plan_passes(const bn_antt_plan* plan) {
 
 // kernel instance per (limbs, role, largest stage field); passes whose stages all use GF(2^8)
 // twiddles have registers to spare for prefetching the next tile
+// next-tile prefetch (BN_PF, persistent grid) is a development-build experiment: the product
+// build does not instantiate those kernels
+#ifdef BN_DEV
+#define BS_KERNEL(R) (pf ? (const void*)antt_bs_pass<L, R, FMAX, true> : (const void*)antt_bs_pass<L, R, FMAX, false>)
+#else
+#define BS_KERNEL(R) ((void)pf, (const void*)antt_bs_pass<L, R, FMAX, false>)
+#endif
 template <int L, int FMAX>
 static const void* kernel_for_f(int role, bool pf) {
 	switch (role) {
-		case ROLE_FIRST: return pf ? (const void*)antt_bs_pass<L, ROLE_FIRST, FMAX, true> : (const void*)antt_bs_pass<L, ROLE_FIRST, FMAX, false>;
-		case ROLE_MID: return pf ? (const void*)antt_bs_pass<L, ROLE_MID, FMAX, true> : (const void*)antt_bs_pass<L, ROLE_MID, FMAX, false>;
-		case ROLE_LAST: return pf ? (const void*)antt_bs_pass<L, ROLE_LAST, FMAX, true> : (const void*)antt_bs_pass<L, ROLE_LAST, FMAX, false>;
-		default: return pf ? (const void*)antt_bs_pass<L, ROLE_SINGLE, FMAX, true> : (const void*)antt_bs_pass<L, ROLE_SINGLE, FMAX, false>;
+		case ROLE_FIRST: return BS_KERNEL(ROLE_FIRST);
+		case ROLE_MID: return BS_KERNEL(ROLE_MID);
+		case ROLE_LAST: return BS_KERNEL(ROLE_LAST);
+		default: return BS_KERNEL(ROLE_SINGLE);
 	}
 }
+#undef BS_KERNEL
 static const void* kernel_for(int L, int role, int fmax, bool pf) {
 	if (L == 4) return fmax <= 8 ? kernel_for_f<4, 8>(role, pf) : kernel_for_f<4, 32>(role, pf);
 	return fmax <= 8 ? kernel_for_f<1, 8>(role, pf) : kernel_for_f<1, 32>(role, pf);
@@ -544,8 +552,6 @@ bool bs_supports(const bn_antt_plan* plan) {
 	return plan->log_h >= kMinLogH && plan->log_h - 5 - kBlkBits <= kMaxOuter && plan->log_rate <= kMaxRateBits;
 }
 
-static int rt_prepare();
-
 int bs_prepare(bn_antt_plan* plan) {
 	for (int L : {1, 4})
 		for (int role = 0; role < 4; role++)
@@ -553,8 +559,7 @@ int bs_prepare(bn_antt_plan* plan) {
 				for (int pf = 0; pf < 2; pf++)
 					BN_HIP(hipFuncSetAttribute(kernel_for(L, role, f, pf != 0), hipFuncAttributeMaxDynamicSharedMemorySize,
 					                           (int)lds_bytes(L)));
-	int rc = rt_prepare();
-	if (rc == BN_OK) rc = rr_prepare(plan);
+	int rc = rr_prepare(plan);
 	if (rc != BN_OK) return rc;
 	int cus = 0;
 	BN_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, plan->device));
@@ -597,13 +602,8 @@ static BsDevKnobs dev_knobs() {
 	return k;
 }
 
-// one launch of pass i of the transform
-static int launch_rt(bn_antt_plan* plan, const BsPass& pass, int i, const uint32_t* d_in, uint32_t* d_out, size_t batch,
-                     hipStream_t st, const BsDevKnobs& kn);
-
 static int launch_one(bn_antt_plan* plan, const BsPass& pass, int i, const uint32_t* d_in, uint32_t* d_out,
                       size_t batch, hipStream_t st, const BsDevKnobs& kn) {
-	if (plan->variant == 2) return launch_rt(plan, pass, i, d_in, d_out, batch, st, kn);
 	// variant 4: every pass on register tiles; variant 5 (mixed): register tiles for the passes whose
 	// twiddles all lie in GF(2^8) (their kernel fits four waves per SIMD), LDS tiles for the others
 	if (plan->variant == 4 || (plan->variant == 5 && pass_fmax(pass) <= 8)) return rr_launch_pass(plan, i, d_in, d_out, batch, st);
@@ -651,19 +651,6 @@ static int launch_one(bn_antt_plan* plan, const BsPass& pass, int i, const uint3
 	return BN_OK;
 }
 
-// pass i of variant 1 alone (variant 3 runs its bottom pass through this kernel: same pass split,
-// same HBM layouts)
-int bs_launch_pass(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st) {
-	size_t n_passes = 0;
-	const BsPass* passes = bs_passes(plan, &n_passes);
-	if (i < 0 || (size_t)i >= n_passes) BN_FAIL(BN_ERR_INVALID, "pass %d out of range", i);
-	const int saved = plan->variant;
-	plan->variant = 1;
-	const int rc = launch_one(plan, passes[i], i, d_in, d_out, batch, st, dev_knobs());
-	plan->variant = saved;
-	return rc;
-}
-
 // the kernel pass i launches under the plan's variant (variants 1, 4, 5), nullptr otherwise
 const void* bs_pass_kernel(bn_antt_plan* plan, int i) {
 	size_t n_passes = 0;
@@ -688,349 +675,6 @@ int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t 
 		if (rc != BN_OK) return rc;
 	}
 	return BN_OK;
-}
-
-// ------------------------------------------------------------------------------------
-// Kernel variant 2: register-resident tiles
-// ------------------------------------------------------------------------------------
-//
-// Same passes, tiles and HBM layouts as variant 1, but the stages run on registers. Wave w of a
-// work-group owns limb plane w of the tile; lane L holds two bitsliced blocks R0, R1 (64 VGPRs).
-// The 7 tile bits are carried by the register index (one bit) and six lane coordinates
-//   c0 = L0^L2, c1 = L1^L2, c2 = L2, c3 = L3, c4 = L4, c5 = L5,
-// whose partner lanes (L ^ 1, 2, 7, 8, 16, 32) are one DPP quad_perm, row_half_mirror or
-// row_ror:8 read, or a gfx950 v_permlane16/32_swap. A stage always pairs R0 with R1 of the same
-// lane: before the stage on tile bit m the register bit is exchanged with lane coordinate m
-// (a transposition: lanes with c_m = 0 keep R0 and take the partner's R0 into R1, lanes with
-// c_m = 1 keep R1 and take the partner's R1 into R0), so the butterfly itself is lane-private
-// (R0 ^= t*R1, R1 ^= R0) and no stage touches LDS. LDS only stages the coalesced tile load
-// and store (and the limb interleave of compact data).
-constexpr int kRtPlane = kTileBlocks * kLimbStride + 32;  // words; the +32 staggers planes by half the banks
-constexpr int kRtOutPlane = 4096 + 256;                    // compact out: element e at e + 4*(e >> 6)
-
-struct RtParams {
-	const uint32_t* src;
-	uint32_t* dst;
-	int log_h, log_rate;
-	unsigned long long* trace;  // development build (BN_DEV) only: per-wave phase timestamps
-	int dbg;                    // development build only: 1 no global loads, 2 no global stores
-	RtPass p;
-};
-
-#ifdef BN_DEV
-#define RT_TS(k)                                                                 \
-	if (P.trace) {                                                               \
-		asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");              \
-		ts[k] = __builtin_amdgcn_s_memtime();                                    \
-	}
-#define RT_DBG(f) (BS_DBG(P) & (f))
-#else
-#define RT_TS(k)
-#define RT_DBG(f) false
-#endif
-
-// Lane-coordinate transposition with the register bit: lanes with c_m = 1 (mk all ones) keep R1
-// and take the partner's R1 into R0, lanes with c_m = 0 keep R0 and take the partner's R0 into R1.
-// The partner read is a ds_bpermute (LDS crossbar, no LDS memory) with a per-lane source address, so
-// one code path serves every coordinate (partner L ^ pi_m) and the identity (pi = 0, mk = 0) the
-// stage on tile bit 6 uses. Selects are v_bitop3 m ? a : b on the lane mask (a C select of two
-// array elements can become a select of their addresses, which would keep R0/R1 out of registers).
-__device__ __forceinline__ void rt_swap(uint32_t* R0, uint32_t* R1, uint32_t mk, int paddr) {
-#pragma unroll
-	for (int i = 0; i < 32; i++) {
-		const uint32_t s = __builtin_amdgcn_bitop3_b32(mk, R0[i], R1[i], 0xca);
-		const uint32_t x = (uint32_t)__builtin_amdgcn_ds_bpermute(paddr, (int)s);
-		R0[i] = __builtin_amdgcn_bitop3_b32(mk, x, R0[i], 0xca);
-		R1[i] = __builtin_amdgcn_bitop3_b32(mk, R1[i], x, 0xca);
-	}
-}
-
-// register arrays are filled and drained component-wise (no uint4 punning, which keeps them out of scratch)
-__device__ __forceinline__ void rt_unpack(uint32_t* r, uint4 v) {
-	r[0] = v.x;
-	r[1] = v.y;
-	r[2] = v.z;
-	r[3] = v.w;
-}
-__device__ __forceinline__ uint4 rt_pack(const uint32_t* r) { return make_uint4(r[0], r[1], r[2], r[3]); }
-
-// Upper passes whose twiddles all lie in GF(2^8) need far fewer registers than the GF(2^32)
-// circuit: they stage the tile through LDS in two halves (37 KB per work-group instead of 74 KB)
-// and run three work-groups per CU, so one work-group's loads and stores overlap the others' stages.
-template <int ROLE, int FMAX>
-struct RtCfg {
-	static constexpr bool LAST = ROLE == ROLE_LAST || ROLE == ROLE_SINGLE;
-	static constexpr bool HALF = !LAST && FMAX <= 8;
-	static constexpr int OCC = HALF ? 3 : 2;
-	static constexpr bool PARK = FMAX > 8;  // idle blocks wait in LDS during the GF(2^16/32) multiplies (register pressure)
-	static constexpr int PLANE = HALF ? (kTileBlocks / 2) * kLimbStride + 32 : kRtPlane;
-};
-
-template <int L, int ROLE, int FMAX>
-__global__ __launch_bounds__(64 * L, (RtCfg<ROLE, FMAX>::OCC)) void antt_rt_pass(RtParams P) {
-	extern __shared__ uint32_t lds[];
-	using C = RtCfg<ROLE, FMAX>;
-	constexpr int NT = 64 * L;
-	constexpr bool IN_COMPACT = ROLE == ROLE_FIRST || ROLE == ROLE_SINGLE;
-	constexpr bool LAST = C::LAST;
-	constexpr bool HALF = C::HALF;
-	constexpr int PL = C::PLANE;
-	const RtPass& ps = P.p;
-	const int tid = threadIdx.x;
-	const int w = tid >> 6, lane = tid & 63;
-	const size_t n = (size_t)1 << P.log_h;
-#ifdef BN_DEV
-	unsigned long long ts[5] = {0, 0, 0, 0, 0};
-#endif
-	RT_TS(0);
-
-	// tile -> (outer bits, coset, batch)
-	const size_t t = blockIdx.x;
-	const size_t outer = t & (((size_t)1 << ps.n_outer) - 1);
-	const size_t rest = t >> ps.n_outer;
-	const int coset = (int)(rest & ((1u << P.log_rate) - 1));
-	const size_t batch = rest >> P.log_rate;
-	size_t ooff = 0;
-	for (int m = 0; m < ps.n_outer; m++) ooff |= ((outer >> m) & 1) << ps.ob[m];
-	uint32_t* dst = P.dst + (((batch << P.log_rate) + (size_t)coset) * n) * L;
-	const uint32_t* src = IN_COMPACT ? (P.src + batch * n * L) : dst;
-	auto tile_off = [&](int q) -> size_t {
-		size_t off = 0;
-#pragma unroll
-		for (int m = 0; m < kBlkBits; m++) off |= (size_t)((q >> m) & 1) << ps.bb[m];
-		return off;
-	};
-	// work-group-uniform twiddle part (outer and coset bits) of stage j, computed once per tile by
-	// lane j; a stage reads it back with v_readlane
-	uint32_t cuv = 0;
-	if (lane < ps.k) {
-		for (int m = 0; m < ps.n_outer; m++)
-			if ((outer >> m) & 1) cuv ^= ps.two[lane][m];
-		for (int b = 0; b < P.log_rate; b++)
-			if ((coset >> b) & 1) cuv ^= ps.twc[lane][b];
-	}
-	auto ucu = [&](int j) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)cuv, j); };
-
-	// ---- coalesced tile load (pieces of 16 B; block q = 32 L words) into LDS planes
-	// (plane l: block q at q * kLimbStride); HALF: blocks with tile bit 6 = h, one half at a time
-	constexpr int NH = HALF ? 2 : 1;
-	constexpr int LPH = kLoads / NH;  // loads per thread per half
-	auto issue = [&](uint4* g, int h) {
-#pragma unroll
-		for (int r = 0; r < LPH; r++) {
-			const int u = tid + r * NT;
-			const int q = h * (kTileBlocks / NH) + u / (8 * L), j = u % (8 * L);
-			g[r] = RT_DBG(1) ? make_uint4(u, j, q, tid) : ld_stream(src + (ooff | tile_off(q)) * L + 4 * j);
-		}
-	};
-	auto to_lds = [&](const uint4* g) {
-#pragma unroll
-		for (int r = 0; r < LPH; r++) {
-			const int u = tid + r * NT;
-			const int lq = u / (8 * L), j = u % (8 * L);
-			if (IN_COMPACT && L > 1) {
-				// compact element j of block q: limb l to plane l, word j
-				const uint32_t v[4] = {g[r].x, g[r].y, g[r].z, g[r].w};
-#pragma unroll
-				for (int l = 0; l < 4; l++) lds[l * PL + lq * kLimbStride + j] = v[l];
-			} else {
-				// bitsliced limb j / 8, words 4 (j % 8).. (or four compact GF(2^32) elements)
-				*(uint4*)(lds + (j >> 3) * PL + lq * kLimbStride + 4 * (j & 7)) = g[r];
-			}
-		}
-	};
-
-	const int c0 = (lane ^ (lane >> 2)) & 1, c1 = ((lane >> 1) ^ (lane >> 2)) & 1;
-	const int G = c0 | (c1 << 1) | (lane & 0x3c);  // lane coordinates c5..c0 as a number
-	const uint32_t* pl = lds + w * PL;
-	uint32_t R0[32], R1[32];
-	// initial mapping: register bit <-> tile bit 6, coordinate c_k <-> tile bit k
-	if (HALF) {
-		uint4 g0[LPH], g1[LPH];
-		issue(g0, 0);
-		issue(g1, 1);
-		to_lds(g0);
-		__syncthreads();
-#pragma unroll
-		for (int i = 0; i < 32; i += 4) rt_unpack(R0 + i, *(const uint4*)(pl + G * kLimbStride + i));
-		__syncthreads();
-		to_lds(g1);
-		__syncthreads();
-#pragma unroll
-		for (int i = 0; i < 32; i += 4) rt_unpack(R1 + i, *(const uint4*)(pl + G * kLimbStride + i));
-	} else {
-		uint4 g[kLoads];
-		issue(g, 0);
-		to_lds(g);
-		__syncthreads();
-#pragma unroll
-		for (int i = 0; i < 32; i += 4) {
-			rt_unpack(R0 + i, *(const uint4*)(pl + G * kLimbStride + i));
-			rt_unpack(R1 + i, *(const uint4*)(pl + (64 + G) * kLimbStride + i));
-		}
-	}
-	if (IN_COMPACT) {
-		transpose32(R0);
-		transpose32(R1);
-	}
-
-	// LDS parking slots of this lane (the staging planes are idle during the stages): blocks at
-	// plane slots L and 64 + L, conflict-free for ds_write_b128 / ds_read_b128
-	__syncthreads();  // every wave has read its input blocks
-	uint32_t* park = lds + w * PL + lane * kLimbStride;
-	RT_TS(1);
-
-	// ---- block stages, tile bit 6 down to mlow
-	// the bottom pass always runs all 7 block stages (mlow = 0); upper passes at least the one on
-	// tile bit 6: a compile-time lower bound keeps the loop from having a zero-trip path
-	const int mlow = LAST ? 0 : ps.mlow;
-#pragma unroll 1
-	for (int m = kBlkBits - 1; m >= mlow; m--) {
-		{
-			// partner lane L ^ pi_m and coordinate c_m = parity(L & kappa_m) (see the table above)
-			const int pi = m == 6 ? 0 : m == 5 ? 32 : m == 4 ? 16 : m == 3 ? 8 : m == 2 ? 7 : m == 1 ? 2 : 1;
-			const int kappa = m == 6 ? 0 : m == 5 ? 32 : m == 4 ? 16 : m == 3 ? 8 : m == 2 ? 4 : m == 1 ? 6 : 5;
-			const uint32_t mk = 0u - (uint32_t)(__builtin_popcount(lane & kappa) & 1);
-			rt_swap(R0, R1, mk, (lane ^ pi) << 2);
-		}
-		uint32_t tw = ucu(ps.jm[m]);
-#pragma unroll
-		for (int b = 0; b < 6; b++) tw ^= ps.tau[m][b] & (0u - (uint32_t)((lane >> b) & 1));
-		uint32_t W[32], Pr[32];
-#pragma unroll
-		for (int i = 0; i < 32; i++) W[i] = (uint32_t)__builtin_amdgcn_sbfe(tw, i, 1);
-		if (C::PARK) {
-			// R0 idles during the multiply: park it in this lane's LDS slot (32 VGPRs for the circuit)
-#pragma unroll
-			for (int i = 0; i < 32; i += 4) *(uint4*)(park + i) = rt_pack(R0 + i);
-		}
-		__builtin_amdgcn_sched_barrier(0);
-		mul_tw<FMAX>(ps.field_m[m], R1, W, Pr);
-		__builtin_amdgcn_sched_barrier(0);
-		if (C::PARK) {
-#pragma unroll
-			for (int i = 0; i < 32; i += 4) rt_unpack(R0 + i, *(const uint4*)(park + i));
-		}
-#pragma unroll
-		for (int i = 0; i < 32; i++) {
-			R0[i] ^= Pr[i];
-			R1[i] ^= R0[i];
-		}
-	}
-
-	RT_TS(2);
-	if (LAST) {
-		// ---- stages 4..0 inside the words. Mapping now: register bit <-> tile bit 0 (index bit 5),
-		// c_k <-> tile bit k + 1. Per stage one multiply serves both blocks: R0's v-lanes move down
-		// onto the u positions, R1's v-lanes stay.
-#pragma unroll 1
-		for (int s = 4; s >= 0; s--) {
-			const int d = 1 << s;
-			const uint32_t um = ~lane_mask(s);
-			uint32_t cb = ucu(s - ps.lo) ^ ps.cb_const[s];
-#pragma unroll
-			for (int b = 0; b < 6; b++) cb ^= ps.tau_iw[s][b] & (0u - (uint32_t)((lane >> b) & 1));
-			uint32_t W[32], T[32];
-#pragma unroll
-			for (int i = 0; i < 32; i++) {
-				T[i] = __builtin_amdgcn_bitop3_b32(R0[i] >> d, R1[i], um, 0xe4);  // (R0>>d & um) | (R1 & ~um)
-				W[i] = ps.pat[s][i] ^ (uint32_t)__builtin_amdgcn_sbfe(cb, i, 1);
-			}
-			// both blocks idle during the multiply: park them in LDS
-#pragma unroll
-			for (int i = 0; i < 32; i += 4) {
-				*(uint4*)(park + i) = rt_pack(R0 + i);
-				*(uint4*)(park + 64 * kLimbStride + i) = rt_pack(R1 + i);
-			}
-			__builtin_amdgcn_sched_barrier(0);
-			mul_tw<FMAX>(ps.field_s[s], T, W, T);
-			__builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-			for (int i = 0; i < 32; i += 4) {
-				rt_unpack(R0 + i, *(const uint4*)(park + i));
-				rt_unpack(R1 + i, *(const uint4*)(park + 64 * kLimbStride + i));
-			}
-#pragma unroll
-			for (int i = 0; i < 32; i++) {
-				const uint32_t a = __builtin_amdgcn_bitop3_b32(T[i], um, R0[i], 0x6a);       // R0 ^ (T & um)
-				const uint32_t b = __builtin_amdgcn_bitop3_b32(T[i] >> d, um, R1[i], 0x6a);  // R1 ^ ((T >> d) & um)
-				R0[i] = __builtin_amdgcn_bitop3_b32(a << d, um, a, 0x9a);                    // a ^ ((a << d) & ~um)
-				R1[i] = __builtin_amdgcn_bitop3_b32(b << d, um, b, 0x9a);
-			}
-		}
-		transpose32(R0);
-		transpose32(R1);
-		RT_TS(3);
-		// lane holds limb w of the 64 consecutive elements 64 G .. 64 G + 63
-		__syncthreads();  // every wave is done with its parking slots
-		uint32_t* op = lds + w * kRtOutPlane;
-#pragma unroll
-		for (int i = 0; i < 32; i += 4) {
-			*(uint4*)(op + G * 68 + i) = rt_pack(R0 + i);
-			*(uint4*)(op + G * 68 + 32 + i) = rt_pack(R1 + i);
-		}
-		__syncthreads();
-		if (L == 4) {
-			for (int e = tid; e < 4096; e += NT) {
-				const int a = e + ((e >> 6) << 2);
-				const uint4 v = make_uint4(lds[a], lds[kRtOutPlane + a], lds[2 * kRtOutPlane + a], lds[3 * kRtOutPlane + a]);
-				if (!RT_DBG(2)) st_stream(dst + (ooff | (size_t)e) * 4, v);
-			}
-		} else {
-			for (int e = 4 * tid; e < 4096; e += 4 * NT) {
-				const int a = e + ((e >> 6) << 2);
-				const uint4 v = *(const uint4*)(lds + a);
-				if (!RT_DBG(2)) st_stream(dst + (ooff | (size_t)e), v);
-			}
-		}
-	} else {
-		// final mapping: register bit <-> tile bit mlow, c_k <-> k (k < mlow) or k + 1 (k >= mlow);
-		// block R_h has tile bit mlow = h and, with that bit removed, local index G
-		auto store_half = [&](int h) {
-#pragma unroll 4
-			for (int r = 0; r < kLoads / 2; r++) {
-				const int u = tid + r * NT;
-				const int lq = u / (8 * L), j = u % (8 * L);
-				const int q = ((lq >> mlow) << (mlow + 1)) | (h << mlow) | (lq & ((1 << mlow) - 1));
-				const uint4 v = *(const uint4*)(lds + (j >> 3) * PL + (HALF ? lq : lq + 64 * h) * kLimbStride + 4 * (j & 7));
-				if (!RT_DBG(2)) st_stream(dst + (ooff | tile_off(q)) * L + 4 * j, v);
-			}
-		};
-		uint32_t* sp = lds + w * PL + G * kLimbStride;
-		__syncthreads();
-		if (HALF) {
-#pragma unroll
-			for (int i = 0; i < 32; i += 4) *(uint4*)(sp + i) = rt_pack(R0 + i);
-			__syncthreads();
-			store_half(0);
-			__syncthreads();
-#pragma unroll
-			for (int i = 0; i < 32; i += 4) *(uint4*)(sp + i) = rt_pack(R1 + i);
-			__syncthreads();
-			store_half(1);
-		} else {
-#pragma unroll
-			for (int i = 0; i < 32; i += 4) {
-				*(uint4*)(sp + i) = rt_pack(R0 + i);
-				*(uint4*)(sp + 64 * kLimbStride + i) = rt_pack(R1 + i);
-			}
-			__syncthreads();
-			store_half(0);
-			store_half(1);
-		}
-		RT_TS(3);
-	}
-	RT_TS(4);
-#ifdef BN_DEV
-	if (P.trace && lane == 0) {
-		unsigned long long* o = P.trace + ((size_t)blockIdx.x * L + w) * 8;
-		o[0] = ts[1] - ts[0];  // load
-		o[1] = ts[2] - ts[1];  // block stages
-		o[2] = ts[3] - ts[2];  // in-word stages + transposes (bottom) / staging out (upper)
-		o[3] = ts[4] - ts[3];  // store
-		o[4] = 1;
-	}
-#endif
 }
 
 // lane bits that lane coordinate c_k depends on
@@ -1082,76 +726,6 @@ int make_rt(const BsPass& p, bool bottom, RtPass* out) {
 		}
 	}
 	*out = r;
-	return BN_OK;
-}
-
-template <int L, int FMAX>
-static const void* rt_kernel_f(int role) {
-	switch (role) {
-		case ROLE_FIRST: return (const void*)antt_rt_pass<L, ROLE_FIRST, FMAX>;
-		case ROLE_MID: return (const void*)antt_rt_pass<L, ROLE_MID, FMAX>;
-		case ROLE_LAST: return (const void*)antt_rt_pass<L, ROLE_LAST, FMAX>;
-		default: return (const void*)antt_rt_pass<L, ROLE_SINGLE, FMAX>;
-	}
-}
-static const void* rt_kernel(int L, int role, int fmax) {
-	if (L == 4) return fmax <= 8 ? rt_kernel_f<4, 8>(role) : fmax <= 16 ? rt_kernel_f<4, 16>(role) : rt_kernel_f<4, 32>(role);
-	return fmax <= 8 ? rt_kernel_f<1, 8>(role) : fmax <= 16 ? rt_kernel_f<1, 16>(role) : rt_kernel_f<1, 32>(role);
-}
-static size_t rt_lds_bytes(int L, int role, int fmax) {
-	const bool last = role == ROLE_LAST || role == ROLE_SINGLE;
-	const int plane = (!last && fmax <= 8) ? RtCfg<ROLE_MID, 8>::PLANE : kRtPlane;
-	return (size_t)L * plane * sizeof(uint32_t);
-}
-
-static int rt_prepare() {
-	for (int L : {1, 4})
-		for (int role = 0; role < 4; role++)
-			for (int f : {8, 16, 32})
-				BN_HIP(hipFuncSetAttribute(rt_kernel(L, role, f), hipFuncAttributeMaxDynamicSharedMemorySize,
-				                           (int)rt_lds_bytes(L, role, f)));
-	return BN_OK;
-}
-
-static int launch_rt(bn_antt_plan* plan, const BsPass& pass, int i, const uint32_t* d_in, uint32_t* d_out, size_t batch,
-                     hipStream_t st, const BsDevKnobs& kn) {
-	const int L = plan->limbs;
-	RtParams prm;
-	prm.src = d_in;
-	prm.dst = d_out;
-	prm.log_h = plan->log_h;
-	prm.log_rate = plan->log_rate;
-	prm.trace = nullptr;
-	prm.dbg = kn.dbg;
-	const bool bottom = pass.role == ROLE_LAST || pass.role == ROLE_SINGLE;
-	int rc = make_rt(pass, bottom, &prm.p);
-	if (rc != BN_OK) BN_FAIL(rc, "register-tile pass table: stage bits are not the top tile bits");
-	const size_t ntiles = (batch << plan->log_rate) << pass.n_outer;
-	static unsigned long long* trbuf = nullptr;
-	if (kn.trace) {
-		if (!trbuf) BN_HIP(hipMalloc(&trbuf, (size_t)1 << 26));
-		BN_HIP(hipMemset(trbuf, 0, ntiles * L * 8 * 8));
-		prm.trace = trbuf;
-	}
-	rc = timing_begin(plan, i, st);
-	if (rc != BN_OK) return rc;
-	void* args[] = {&prm};
-	const int fmax = pass_fmax(pass);
-	BN_HIP(hipLaunchKernel(rt_kernel(L, pass.role, fmax), dim3((unsigned)ntiles), dim3(64 * L), args, rt_lds_bytes(L, pass.role, fmax), st));
-	rc = timing_end(plan, i, st);
-	if (rc != BN_OK) return rc;
-	if (prm.trace) {
-		const size_t g = ntiles * (size_t)L;
-		std::vector<unsigned long long> h(g * 8);
-		BN_HIP(hipStreamSynchronize(st));
-		BN_HIP(hipMemcpy(h.data(), prm.trace, g * 8 * 8, hipMemcpyDeviceToHost));
-		double acc[8] = {0};
-		for (size_t w = 0; w < g; w++)
-			for (int k = 0; k < 8; k++) acc[k] += (double)h[w * 8 + k];
-		const double t = acc[4] > 0 ? acc[4] : 1;
-		fprintf(stderr, "trace rt pass %d (fmax %d, %zu wave-tiles, cycles per wave-tile): load %.0f  block %.0f  inword/stage-out %.0f  store %.0f\n",
-		        i, fmax, (size_t)acc[4], acc[0] / t, acc[1] / t, acc[2] / t, acc[3] / t);
-	}
 	return BN_OK;
 }
 

@@ -1,5 +1,5 @@
-// Shared pass tables of the bitsliced additive-NTT kernels (antt_bs.hip variants 1/2, antt_rr.hip
-// variant 4): tiles of 128 bitsliced 32-element blocks, host-tabulated twiddle contributions.
+// Shared pass tables of the bitsliced additive-NTT kernels (antt_bs.hip variant 1, antt_rr.hip
+// variant 4; variant 5 = both): tiles of 128 bitsliced 32-element blocks, host-tabulated twiddle contributions.
 #pragma once
 
 #include <stdint.h>
@@ -32,7 +32,7 @@ struct BsPass {
 	uint32_t pat[5][32];                     // stages 0..4: bit-lane part of the twiddle words
 };
 
-// Register-tile pass table (variants 2 and 4): wave w owns limb plane w of the tile; lane L holds two
+// Register-tile pass table (variant 4): wave w owns limb plane w of the tile; lane L holds two
 // blocks R0, R1; the 7 tile bits are the register index plus six lane coordinates
 //   c0 = L0^L2, c1 = L1^L2, c2 = L2, c3 = L3, c4 = L4, c5 = L5
 // (partner lanes L ^ 1, 2, 7, 8, 16, 32). Before the stage on tile bit m < 6 the register bit is
@@ -57,7 +57,6 @@ const BsPass* bs_passes(bn_antt_plan* plan, size_t* n_passes);
 int pass_fmax(const BsPass& p);
 // register-tile table of a pass; BN_ERR_UNSUPPORTED when the stage bits are not the top tile bits
 int make_rt(const BsPass& p, bool bottom, RtPass* out);
-int bs_launch_pass(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st);
 // variant 4 (antt_rr.hip): register-tile kernels over the same passes
 int rr_prepare(bn_antt_plan* plan);
 int rr_launch_pass(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st);

@@ -22,9 +22,6 @@ struct bn_antt_plan {
 	uint32_t* scratch = nullptr;   // pass-intermediate buffer (variant-specific)
 	size_t scratch_bytes = 0;
 	std::vector<unsigned char> bs_passes;  // variant-1 pass tables (antt_bs.hip), built on first use
-	std::vector<unsigned char> rd_host;    // variant-3 pass tables (antt_rd.hip), host copy
-	void* rd_tables = nullptr;             // ... and the device copy the kernels read
-	int rd_n_passes = 0;
 	hipStream_t own_stream = nullptr;
 	// host-apply staging
 	void* h_dev_in = nullptr;

@@ -42,7 +42,9 @@ public:
 		ulvt::bn_check(bn_antt_forward_device(plan, d_in, d_out, batch, stream));
 	}
 
-	// 0: compact tiles, per-butterfly twiddles; 1: bitsliced tiles (default for log_h >= 12)
+	// 0: compact tiles, per-butterfly twiddles (default for log_h < 12); 1: bitsliced LDS tiles;
+	// 4: bitsliced register tiles; 5: 4 for the GF(2^8)-twiddle passes, 1 for the others (default
+	// for log_h >= 12)
 	void set_variant(int variant) { ulvt::bn_check(bn_antt_plan_set_variant(plan, variant)); }
 
 	const AdditiveNTTConf<T, P>& conf() const { return ntt_conf; }

@@ -275,10 +275,9 @@ class AdditiveNTT:
 
     def set_variant(self, variant):
         """0: compact tiles, per-butterfly twiddles (default for log_h < 12); 1: bitsliced LDS tiles;
-        2: bitsliced register tiles with LDS exchanges; 3: round-scheduled bitsliced tiles
-        (log_rate <= 4); 4: register tiles (three to four waves per SIMD) on every pass; 5: register
-        tiles for the GF(2^8)-twiddle passes, LDS tiles for the others (default for log_h >= 12).
-        Variants 1-5 need log_h >= 12; results are identical."""
+        4: bitsliced register tiles (three to four waves per SIMD) on every pass; 5: register tiles
+        for the GF(2^8)-twiddle passes, LDS tiles for the others (default for log_h >= 12).
+        Variants 1, 4 and 5 need log_h >= 12; results are identical."""
         _check(lib().bn_antt_plan_set_variant(self._plan, variant))
 
     def set_event_timing(self, enable):

@@ -78,11 +78,10 @@ int bn_antt_plan_query(const bn_antt_plan* plan, int what, int64_t* value);
 /* Kernel selection, the analogue of choosing AdditiveNTT vs ModifiedAdditiveNTT
  * (src/ulvt/ntt/modified_antt.cuh:223-427, benchmark_antt.cu): 0 = compact tiles with the twiddle
  * recomputed per butterfly from the subspace table (the reference kernel's scheme), 1 = bitsliced
- * LDS tiles with host-tabulated twiddle contributions, 2 = the same passes with register-resident
- * tiles (LDS exchanges), 3 = round-scheduled bitsliced tiles (log_rate <= 4), 4 = register tiles
- * sized for three to four waves per SIMD on every pass, 5 = variant 4 for the passes whose
- * twiddles all lie in GF(2^8) and variant 1 for the others (default when log_h >= 12; DESIGN.md
- * section 5.1). Variants 1-5 need log_h >= 12; results are identical. */
+ * LDS tiles with host-tabulated twiddle contributions, 4 = bitsliced register tiles (three to four
+ * waves per SIMD) on every pass, 5 = variant 4 for the passes whose twiddles all lie in GF(2^8)
+ * and variant 1 for the others (default when log_h >= 12). Other values
+ * return BN_ERR_INVALID. Variants 1, 4 and 5 need log_h >= 12; results are identical. */
 int bn_antt_plan_set_variant(bn_antt_plan* plan, int variant);
 
 /* Profiling hook for bench.py: records hipEvents around every kernel launch of the next
@@ -93,13 +92,13 @@ int bn_antt_get_event_timing(bn_antt_plan* plan, float* ms_per_kind, int max_kin
  * launched `reps` times back to back on `stream` between two hipEvents, giving its steady-state
  * duration per launch in ms_per_pass[pass]. d_out's contents are meaningless afterwards (passes
  * are re-applied to their own output; their cost does not depend on the values). Variants
- * 1-5. Synchronous. */
+ * 1, 4 and 5. Synchronous. */
 int bn_antt_time_passes(bn_antt_plan* plan, const void* d_in, void* d_out, size_t batch, int reps,
                         void* stream, float* ms_per_pass, int max_passes, int* n_passes);
 /* Profiling (no reference counterpart): the demangled name of the kernel that pass `pass` of the
  * plan's current variant launches, as rocprofv3 reports it (e.g. "void bn::antt_bs_pass<4, 2, 32,
  * false>(bn::BsParams)"), so committed counter summaries can be matched to the launches exactly.
- * BN_ERR_UNSUPPORTED for variants 0, 2 and 3. */
+ * BN_ERR_UNSUPPORTED for variant 0. */
 int bn_antt_pass_kernel_name(bn_antt_plan* plan, int pass, char* buf, size_t cap);
 
 /* ------------------------------------------------------------------------------------

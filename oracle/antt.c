@@ -14,6 +14,7 @@
  */
 #define _POSIX_C_SOURCE 200809L
 #include <pthread.h>
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -187,21 +188,37 @@ void orc_antt128_limbwise(const uint32_t* in, uint32_t* out, int log_h, int log_
 /*
  * All-cores CPU baseline (bench.py cpu_baseline): the same serial algorithm as
  * orc_antt128_limbwise, with the butterflies of each stage split into contiguous ranges over
- * `nthreads` pthreads (a barrier between stages, as the reference's kernel launches are).
+ * worker threads (a barrier between stages, as the reference's kernel launches are). The workers
+ * are a persistent pool, created on first use and reused by every later call and stage, and a
+ * call uses at most one thread per kMinBfPerThread butterflies of a stage (orc_antt_mt_threads),
+ * so a small transform is not timed as thread start-up and barrier traffic.
  * Flattened butterfly t of a stage: blk = t >> stage, k = t & (2^stage - 1).
  */
+enum { kMinBfPerThread = 1 << 12, kPoolMax = 256 };
+
 typedef struct {
 	const uint32_t* s;
 	uint32_t* d;
-	int width, log_h, log_rate, coset, nthreads, id;
-	pthread_barrier_t* bar;
-} mt_arg;
+	int width, log_h, log_rate, coset, nthreads;
+} mt_job;
 
-static void* mt_worker(void* p) {
-	mt_arg* a = (mt_arg*)p;
+static struct {
+	pthread_mutex_t mu;
+	pthread_cond_t start, done;
+	pthread_t th[kPoolMax];
+	int size;            /* threads in the pool, the caller included */
+	unsigned long gen;   /* job generation */
+	int pending;         /* workers of the current job still running */
+	const mt_job* job;   /* valid until pending reaches 0 */
+	int job_n;           /* its thread count (read under the lock: late non-participants never touch job) */
+	pthread_barrier_t bar;
+	int bar_n;           /* participants the stage barrier is set up for (0: none) */
+} pool = {.mu = PTHREAD_MUTEX_INITIALIZER, .start = PTHREAD_COND_INITIALIZER, .done = PTHREAD_COND_INITIALIZER};
+
+static void mt_run(const mt_job* a, int id) {
 	const size_t n = (size_t)1 << a->log_h;
 	const size_t nbf = n / 2;
-	const size_t lo = nbf * (size_t)a->id / (size_t)a->nthreads, hi = nbf * (size_t)(a->id + 1) / (size_t)a->nthreads;
+	const size_t lo = nbf * (size_t)id / (size_t)a->nthreads, hi = nbf * (size_t)(id + 1) / (size_t)a->nthreads;
 	for (int stage = a->log_h - 1; stage >= 0; stage--) {
 		const size_t half = (size_t)1 << stage;
 		size_t cur_blk = (size_t)-1;
@@ -219,34 +236,78 @@ static void* mt_worker(void* p) {
 				v[q] ^= u[q];
 			}
 		}
-		pthread_barrier_wait(a->bar);
+		if (a->nthreads > 1) pthread_barrier_wait(&pool.bar);
+	}
+}
+
+static void* pool_worker(void* p) {
+	const int id = (int)(intptr_t)p;
+	unsigned long seen = 0;
+	for (;;) {
+		pthread_mutex_lock(&pool.mu);
+		while (pool.gen == seen) pthread_cond_wait(&pool.start, &pool.mu);
+		seen = pool.gen;
+		const mt_job* job = pool.job;
+		const int n = pool.job_n;
+		pthread_mutex_unlock(&pool.mu);
+		if (id < n) {
+			mt_run(job, id);
+			pthread_mutex_lock(&pool.mu);
+			if (--pool.pending == 0) pthread_cond_signal(&pool.done);
+			pthread_mutex_unlock(&pool.mu);
+		}
 	}
 	return NULL;
 }
 
+int orc_antt_mt_threads(int log_h, int nthreads) {
+	const size_t nbf = ((size_t)1 << log_h) / 2;
+	size_t cap = nbf / kMinBfPerThread;
+	if (cap < 1) cap = 1;
+	if (nthreads < 1) nthreads = 1;
+	if (nthreads > kPoolMax) nthreads = kPoolMax;
+	return (size_t)nthreads > cap ? (int)cap : nthreads;
+}
+
 void orc_antt128_limbwise_mt(const uint32_t* in, uint32_t* out, int log_h, int log_rate, int nthreads) {
 	orc_init();
-	if (nthreads < 1) nthreads = 1;
+	nthreads = orc_antt_mt_threads(log_h, nthreads);
 	const int width = log_h + log_rate - 1;
 	uint32_t* s = (uint32_t*)calloc((size_t)log_h * (size_t)(width > 0 ? width : 1), sizeof(uint32_t));
 	orc_subspace_evals32(log_h, log_rate, s);
 	const size_t n = (size_t)1 << log_h;
-	if ((size_t)nthreads > n / 2) nthreads = (int)(n / 2 > 0 ? n / 2 : 1);
-	pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
-	mt_arg* args = (mt_arg*)calloc((size_t)nthreads, sizeof(mt_arg));
-	pthread_barrier_t bar;
+	pthread_mutex_lock(&pool.mu);
+	if (pool.size == 0) pool.size = 1;  /* the caller is thread 0 */
+	while (pool.size < nthreads) {
+		pthread_create(&pool.th[pool.size], NULL, pool_worker, (void*)(intptr_t)pool.size);
+		pool.size++;
+	}
+	if (nthreads > 1 && pool.bar_n != nthreads) {
+		/* no job is running (calls are serialised by the caller), so the barrier is idle */
+		if (pool.bar_n) pthread_barrier_destroy(&pool.bar);
+		pthread_barrier_init(&pool.bar, NULL, (unsigned)nthreads);
+		pool.bar_n = nthreads;
+	}
+	pthread_mutex_unlock(&pool.mu);
 	for (int c = 0; c < (1 << log_rate); c++) {
 		uint32_t* d = out + 4 * (size_t)c * n;
 		memcpy(d, in, 4 * n * sizeof(uint32_t));
-		pthread_barrier_init(&bar, NULL, (unsigned)nthreads);
-		for (int i = 0; i < nthreads; i++) {
-			args[i] = (mt_arg){s, d, width, log_h, log_rate, c, nthreads, i, &bar};
-			pthread_create(&th[i], NULL, mt_worker, &args[i]);
+		const mt_job job = {s, d, width, log_h, log_rate, c, nthreads};
+		if (nthreads > 1) {
+			pthread_mutex_lock(&pool.mu);
+			pool.job = &job;
+			pool.job_n = nthreads;
+			pool.pending = nthreads - 1;
+			pool.gen++;
+			pthread_cond_broadcast(&pool.start);
+			pthread_mutex_unlock(&pool.mu);
 		}
-		for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
-		pthread_barrier_destroy(&bar);
+		mt_run(&job, 0);
+		if (nthreads > 1) {
+			pthread_mutex_lock(&pool.mu);
+			while (pool.pending > 0) pthread_cond_wait(&pool.done, &pool.mu);
+			pthread_mutex_unlock(&pool.mu);
+		}
 	}
-	free(args);
-	free(th);
 	free(s);
 }

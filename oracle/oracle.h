@@ -64,6 +64,9 @@ void orc_antt128_limbwise(const uint32_t* in, uint32_t* out, int log_h, int log_
  * element stride 4 words, transform stride 4 << log_h words.                  */
 void orc_antt128_limbwise_batch(const uint32_t* in, uint32_t* out, int log_h, int log_rate, int batch);
 void orc_antt128_limbwise_mt(const uint32_t* in, uint32_t* out, int log_h, int log_rate, int nthreads);
+/* Threads orc_antt128_limbwise_mt actually uses for a 2^log_h transform when asked for nthreads
+ * (at most one per 4096 butterflies of a stage; persistent pool, at most 256). */
+int orc_antt_mt_threads(int log_h, int nthreads);
 
 /* ---------------- bitslicing (src/ulvt/utils/bitslicing.cuh:32-74) ---------------- */
 void orc_bitslice_transpose128(uint32_t blk[128]);

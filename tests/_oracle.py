@@ -46,6 +46,8 @@ def lib():
             getattr(L, fn).argtypes = [_u32p, _u32p, ctypes.c_int, ctypes.c_int]
         L.orc_antt128_limbwise_mt.restype = None
         L.orc_antt128_limbwise_mt.argtypes = [_u32p, _u32p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.orc_antt_mt_threads.restype = ctypes.c_int
+        L.orc_antt_mt_threads.argtypes = [ctypes.c_int, ctypes.c_int]
         L.orc_antt128_limbwise_batch.argtypes = [_u32p, _u32p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         for fn in ("orc_bitslice_transpose128", "orc_bitslice_untranspose128",
                    "orc_bitslice_transpose32", "orc_bitslice_untranspose32"):

@@ -119,10 +119,14 @@ def test_fold_multilinear_matches_lagrange_sum(n, d):
 
 def test_multithreaded_ntt_matches_serial():
     L = O.lib()
-    for log_h in (1, 6, 13):
+    # at most one thread per 4096 butterflies of a stage (a small transform runs on one thread)
+    assert L.orc_antt_mt_threads(10, 16) == 1
+    assert L.orc_antt_mt_threads(15, 3) == 3 and L.orc_antt_mt_threads(15, 8) == 4
+    assert L.orc_antt_mt_threads(24, 16) == 16 and L.orc_antt_mt_threads(24, 0) == 1
+    for log_h, r in ((1, 0), (6, 0), (13, 0), (15, 0), (16, 1)):
         x = O.fill128(11 + log_h, 12, 1 << log_h)
-        want = O.antt128(x, log_h, 0)
-        for nt in (1, 3, 8):
+        want = O.antt128(x, log_h, r)
+        for nt in (1, 3, 8, 2):  # the persistent pool grows, then serves a smaller count
             out = np.zeros_like(want)
-            L.orc_antt128_limbwise_mt(x.reshape(-1), out.reshape(-1), log_h, 0, nt)
-            assert np.array_equal(out, want), (log_h, nt)
+            L.orc_antt128_limbwise_mt(x.reshape(-1), out.reshape(-1), log_h, r, nt)
+            assert np.array_equal(out, want), (log_h, r, nt)
