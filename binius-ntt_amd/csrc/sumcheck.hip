@@ -97,6 +97,7 @@ struct ScArgs {
 	uint32_t* acc;      // kAccCopies x (kmax + 1) x 4 words, XOR-accumulated (this round's set)
 	uint32_t* clr;      // the other accumulator set: cleared here for the next round
 	uint32_t* res;      // host-mapped: 4 (kMaxD + 1) point words, then the sequence word
+	uint32_t* sink;     // optional device copy of the raw point words + flags (bn_sumcheck_set_message_sink)
 	uint32_t seq;       // this launch's sequence number
 	int post;           // 1: the last workgroup posts the points (small grids), 0: sc_post does
 	uint32_t kcol[kMaxD + 1][4];  // GF(2^4) products k * 2^a (interpolation point k)
@@ -152,7 +153,9 @@ __device__ __forceinline__ void post_points(const ScArgs& A, int t) {
 		for (int c = 0; c < kAccCopies; c++)
 			v ^= __hip_atomic_load(A.acc + c * kAccStride + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		A.res[t] = v;
+		if (A.sink) A.sink[t] = v;
 	}
+	if (A.sink && t == 0) A.sink[kResSeq] = (uint32_t)A.skip1 | (A.mode == 2 ? 2u : 0u);
 	__threadfence_system();
 	__syncthreads();
 	if (t == 0) __hip_atomic_store(A.res + kResSeq, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -241,7 +244,11 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_messages(ScArgs A) {
 		return;  // sc_post follows
 	}
 	if (gridDim.x == 1) {  // a single workgroup posts its own sums
-		if (threadIdx.x < 4 * (A.kmax + 1)) A.res[threadIdx.x] = accL[threadIdx.x];
+		if (threadIdx.x < 4 * (A.kmax + 1)) {
+			A.res[threadIdx.x] = accL[threadIdx.x];
+			if (A.sink) A.sink[threadIdx.x] = accL[threadIdx.x];
+		}
+		if (A.sink && threadIdx.x == 0) A.sink[kResSeq] = (uint32_t)A.skip1 | (A.mode == 2 ? 2u : 0u);
 		__threadfence_system();
 		__syncthreads();
 		if (threadIdx.x == 0) __hip_atomic_store(A.res + kResSeq, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -379,10 +386,15 @@ struct bn_sumcheck {
 	uint32_t* acc = nullptr;    // 2 sets of kAccSet words (see kAccCopies), alternating rounds
 	int par = 0;                // set used by the next round_messages
 	uint32_t* h_res = nullptr;  // host-mapped, GPU-coherent: the round's points + sequence word
+	uint32_t* sink = nullptr;   // caller's device buffer for the raw point words (sharded exchange)
 	uint32_t* d_res = nullptr;  // its device address
 	uint32_t seq = 0;
 	hipStream_t stream = nullptr;
 	bool sharded_used = false;
+	// bn_sumcheck_create_staged leaves compact input untransposed until bn_sumcheck_prepare (the
+	// reference constructor's separate Memcpy and Transpose phases, sumcheck.cuh:88-124)
+	bool prepared = true;
+	int compact_input = 0;
 	// Round claim: once round i's points are known, move_to_next_round(r) interpolates them at r,
 	// which is this prover's sum for round i + 1 (p_i(r) = sum_x prod_j f_j'(x), per shard too).
 	// Round i + 1 then skips point 1 (p(1) = claim + p(0)): (d - 1) fewer products per pair.
@@ -426,6 +438,7 @@ int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 	}
 	A.skip1 = (!fold && (sc->have_claim || sc->claim_pending) && A.mode != 2) ? 1 : 0;
 	A.res = sc->d_res;
+	A.sink = fold ? nullptr : sc->sink;
 	if (!fold) A.seq = ++sc->seq;
 	A.acc = sc->acc + kAccSet * sc->par;
 	A.clr = sc->acc + kAccSet * (1 - sc->par);
@@ -513,25 +526,39 @@ int check_shape(int num_vars, int d, int transposed) {
 	return BN_OK;
 }
 
-// Common tail of both constructors: `stage` holds the d columns back to back (4*2^n words
-// each, compact or bitsliced); it becomes the prover's storage (converted in place).
-int sc_finish_create(bn_sumcheck* sc, int transposed) {
-	const size_t n = (size_t)1 << sc->num_vars;
-	if (!transposed) {
+// Device bit-transpose of compact input (the reference constructor's transpose_kernel,
+// sumcheck.cuh:97-101), then a stream synchronisation: the prover is ready for round 0.
+int sc_prepare(bn_sumcheck* sc) {
+	if (sc->prepared) return BN_OK;
+	if (sc->compact_input) {
 		const size_t blocks = sc->col_words / 128 * (size_t)sc->d;
 		int rc = bn_bitslice_device(sc->cols, blocks, 0, sc->stream);
 		if (rc != BN_OK) return rc;
 	}
+	BN_HIP(hipStreamSynchronize(sc->stream));
+	sc->prepared = true;
+	return BN_OK;
+}
+
+// Common tail of both constructors: the d columns (4*2^n words each, compact or bitsliced) are in
+// the prover's storage; compact ones are converted in place unless `stage_only`.
+int sc_finish_create(bn_sumcheck* sc, int transposed, bool stage_only = false) {
+	const size_t n = (size_t)1 << sc->num_vars;
+	sc->compact_input = !transposed;
+	sc->prepared = false;
 	sc->cur = n;
 	sc->round = 0;
-	BN_HIP(hipStreamSynchronize(sc->stream));
-	return BN_OK;
+	if (stage_only) {
+		BN_HIP(hipStreamSynchronize(sc->stream));
+		return BN_OK;
+	}
+	return sc_prepare(sc);
 }
 
 }  // namespace
 
-extern "C" int bn_sumcheck_create(int device, int num_vars, int d, int transposed, const uint32_t* evals,
-								  bn_sumcheck** out) {
+static int create_from_host(int device, int num_vars, int d, int transposed, const uint32_t* evals, bool stage_only,
+                            bn_sumcheck** out) {
 	BN_CHECK_ARG(out, "NULL output pointer");
 	*out = nullptr;
 	BN_CHECK_ARG(evals, "NULL evals");
@@ -559,12 +586,28 @@ extern "C" int bn_sumcheck_create(int device, int num_vars, int d, int transpose
 		sc_free(sc);
 		BN_FAIL(BN_ERR_HIP, "copying evals to the device: %s", hipGetErrorString(e));
 	}
-	if ((rc = sc_finish_create(sc, transposed)) != BN_OK) {
+	if ((rc = sc_finish_create(sc, transposed, stage_only)) != BN_OK) {
 		sc_free(sc);
 		return rc;
 	}
 	*out = sc;
 	return BN_OK;
+}
+
+extern "C" int bn_sumcheck_create(int device, int num_vars, int d, int transposed, const uint32_t* evals,
+								  bn_sumcheck** out) {
+	return create_from_host(device, num_vars, d, transposed, evals, false, out);
+}
+
+extern "C" int bn_sumcheck_create_staged(int device, int num_vars, int d, int transposed, const uint32_t* evals,
+                                         bn_sumcheck** out) {
+	return create_from_host(device, num_vars, d, transposed, evals, true, out);
+}
+
+extern "C" int bn_sumcheck_prepare(bn_sumcheck* sc) {
+	BN_CHECK_ARG(sc, "NULL prover");
+	DeviceScope ds(sc->device);
+	return sc_prepare(sc);
 }
 
 extern "C" int bn_sumcheck_create_device(int device, int num_vars, int d, int transposed, void* d_evals, int take,
@@ -684,6 +727,10 @@ extern "C" int bn_sumcheck_set_shard(bn_sumcheck* sc, int rank, int world) {
 	BN_CHECK_ARG(n >= (size_t)32 * world, "need at least one 32-element batch per rank");
 	if (world == 1) return BN_OK;
 	DeviceScope ds(sc->device);
+	if (!sc->prepared) {  // a staged prover transposes on first use
+		const int prc = sc_prepare(sc);
+		if (prc != BN_OK) return prc;
+	}
 	// keep the batches b with b mod world == rank, in order
 	const size_t nb_local = n / 32 / world;
 	uint32_t* local = nullptr;
@@ -751,10 +798,26 @@ extern "C" int bn_sumcheck_import_gathered(bn_sumcheck* sc, const uint32_t* word
 	return BN_OK;
 }
 
+extern "C" int bn_sumcheck_set_message_sink(bn_sumcheck* sc, void* d_words) {
+	BN_CHECK_ARG(sc, "NULL prover");
+	sc->sink = (uint32_t*)d_words;
+	return BN_OK;
+}
+
+extern "C" int bn_sumcheck_stream(const bn_sumcheck* sc, void** stream) {
+	BN_CHECK_ARG(sc && stream, "NULL argument");
+	*stream = (void*)sc->stream;
+	return BN_OK;
+}
+
 extern "C" int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32_t* points) {
 	BN_CHECK_ARG(sc && sum && points, "NULL argument");
 	BN_CHECK_ARG(!(sc->world > 1 && sc->cur <= 32), "shard exhausted: gather (export_shard/import_gathered) first");
 	DeviceScope ds(sc->device);
+	if (!sc->prepared) {  // a staged prover transposes on first use
+		const int prc = sc_prepare(sc);
+		if (prc != BN_OK) return prc;
+	}
 	if (!sc->msgs_queued) {
 		int rc = queue_messages(sc);
 		if (rc != BN_OK) return rc;
@@ -812,6 +875,10 @@ extern "C" int bn_sumcheck_move_to_next_round(bn_sumcheck* sc, const uint32_t* c
 	BN_CHECK_ARG(sc->cur >= 2, "no variables left to fold");
 	BN_CHECK_ARG(!(sc->world > 1 && sc->cur <= 32), "shard exhausted: gather (export_shard/import_gathered) first");
 	DeviceScope ds(sc->device);
+	if (!sc->prepared) {  // a staged prover transposes on first use
+		const int prc = sc_prepare(sc);
+		if (prc != BN_OK) return prc;
+	}
 	int rc = sc_launch(sc, true, challenge);
 	if (rc != BN_OK) return rc;
 	// no sync: the fold is ordered before the next round's messages on the prover's stream

@@ -81,12 +81,16 @@ def lib():
         "bn_packed32_device": (i32, [i32, i32, vp, vp, vp, vp, sz, vp]),
         "bn_sumcheck_create": (i32, [i32, i32, i32, i32, u32p, ctypes.POINTER(vp)]),
         "bn_sumcheck_create_device": (i32, [i32, i32, i32, i32, vp, i32, ctypes.POINTER(vp)]),
+        "bn_sumcheck_create_staged": (i32, [i32, i32, i32, i32, u32p, ctypes.POINTER(vp)]),
+        "bn_sumcheck_prepare": (i32, [vp]),
         "bn_sumcheck_round_messages": (i32, [vp, u32p, u32p]),
         "bn_sumcheck_move_to_next_round": (i32, [vp, u32p]),
         "bn_sumcheck_round": (i32, [vp, ctypes.POINTER(i32)]),
         "bn_sumcheck_set_shard": (i32, [vp, i32, i32]),
         "bn_sumcheck_create_shard_device": (i32, [i32, i32, i32, i32, i32, vp, vp, ctypes.POINTER(vp)]),
         "bn_sumcheck_needs_gather": (i32, [vp, ctypes.POINTER(i32)]),
+        "bn_sumcheck_set_message_sink": (i32, [vp, vp]),
+        "bn_sumcheck_stream": (i32, [vp, ctypes.POINTER(vp)]),
         "bn_sumcheck_export_shard": (i32, [vp, u32p, sz]),
         "bn_sumcheck_import_gathered": (i32, [vp, u32p, sz, i32]),
         "bn_sumcheck_destroy": (i32, [vp]),
@@ -500,13 +504,17 @@ def packed32_device(op, height, a, b=None, c=None, d=None, stream=None):
 class Sumcheck:
     """Sumcheck<NUM_VARS, COMPOSITION_SIZE, DATA_IS_TRANSPOSED> (sumcheck.cuh:10-301)."""
 
-    def __init__(self, num_vars, composition_size, data_is_transposed, evals, device=0, shard=None):
+    def __init__(self, num_vars, composition_size, data_is_transposed, evals, device=0, shard=None, staged=False):
+        """staged=True (host evals only): copy the columns but leave compact input untransposed until
+        prepare() (or the first round) — the reference constructor's separate Memcpy and Transpose
+        phases (sumcheck.cuh:88-124)."""
         self.num_vars, self.d = num_vars, composition_size
         p = ctypes.c_void_p()
         if isinstance(evals, np.ndarray):
             ev = np.ascontiguousarray(evals, dtype=np.uint32).reshape(-1)
-            _check(lib().bn_sumcheck_create(device, num_vars, composition_size, 1 if data_is_transposed else 0,
-                                            ev.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(p)))
+            create = lib().bn_sumcheck_create_staged if staged else lib().bn_sumcheck_create
+            _check(create(device, num_vars, composition_size, 1 if data_is_transposed else 0,
+                          ev.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(p)))
         else:
             _check_device_tensor(evals, composition_size * 4 << num_vars, "evals")
             # the library copies on its own stream: the producer (an NTT, a torch kernel) must be done.
@@ -520,6 +528,10 @@ class Sumcheck:
         self._bind()
         if shard is not None:
             _check(lib().bn_sumcheck_set_shard(self._sc, shard[0], shard[1]))
+
+    def prepare(self):
+        """The device bit-transpose of a staged prover's compact columns (synchronous; no-op otherwise)."""
+        _check(lib().bn_sumcheck_prepare(self._sc))
 
     def _bind(self):
         # per-round calls are on the protocol's critical path (the GPU waits for the host's
@@ -573,6 +585,23 @@ class Sumcheck:
         return r.value
 
     # sharded endgame (see bn_sumcheck_needs_gather); driven by binius_ntt_amd.distributed
+    def set_message_sink(self, words):
+        """bn_sumcheck_set_message_sink: later messages kernels also write the raw point words (and
+        the p(1)-skipped flag at word 36) into `words`, a device tensor of >= 37 int32 (None: stop)."""
+        if words is None:
+            _check(lib().bn_sumcheck_set_message_sink(self._sc, None))
+            self._sink = None
+            return
+        _check_device_tensor(words, 4 * (8 + 1) + 1, "message sink")
+        self._sink = words  # keep the buffer alive while the prover writes it
+        _check(lib().bn_sumcheck_set_message_sink(self._sc, _ptr(words)))
+
+    def stream_handle(self):
+        """The prover's hipStream_t (as an int), for torch.cuda.ExternalStream."""
+        s = ctypes.c_void_p()
+        _check(lib().bn_sumcheck_stream(self._sc, ctypes.byref(s)))
+        return s.value or 0
+
     def needs_gather(self):
         f = ctypes.c_int()
         _check(lib().bn_sumcheck_needs_gather(self._sc, ctypes.byref(f)))

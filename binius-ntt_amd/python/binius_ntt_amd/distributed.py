@@ -91,18 +91,47 @@ def xor_allreduce_words(words, group=None):
     return np.bitwise_xor.reduce(g, axis=0)
 
 
-class ShardedSumcheck:
-    """Drives a sharded prover so that every rank sees the global round messages."""
+SINK_WORDS = 40  # bn_sumcheck_set_message_sink: 4 * (8 + 1) point words, the p(1)-skipped flag at 36
 
-    def __init__(self, prover, group=None):
+
+class ShardedSumcheck:
+    """Drives a sharded prover so that every rank sees the global round messages.
+
+    Exchange paths for the per-round (sum, points) words:
+      * device (default on an nccl group with a HIP prover): the prover's messages kernel also writes
+        its raw partial points into a preallocated device sink (bn_sumcheck_set_message_sink), the
+        current stream waits for the prover's stream, `all_gather_into_tensor` reads the sink
+        directly and one copy brings the world x 40 words back; the partial points are XOR-ed and
+        p(1), sum are completed from the GLOBAL claim (p(1) = claim + p(0), sum = claim, the claim
+        being the previous round's global points interpolated at its challenge) — so no
+        numpy -> pinned -> H2D hop per round;
+      * host (gloo, or a prover without a sink): the words the prover returned are staged through
+        WordExchange.
+    exchange_at_world1=True runs the exchange even when the group has one rank (the RCCL rehearsal
+    on a one-GPU box exercises the device path that way)."""
+
+    def __init__(self, prover, group=None, device_exchange=None, exchange_at_world1=False):
         import torch.distributed as dist
         self.prover = prover
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.replicated = self.world == 1  # after the endgame gather every rank holds everything
+        self.replicated = self.world == 1 and not exchange_at_world1  # after the endgame gather every rank holds everything
         self._msg = None  # WordExchange for the (d + 2) x 4 message words, built on first use
         self.exchange_seconds = 0.0  # per-round message exchanges + the endgame gather
         self.exchange_rounds = 0
+        if device_exchange is None:
+            device_exchange = dist.is_initialized() and dist.get_backend(group) == "nccl"
+        self.device_exchange = bool(device_exchange) and hasattr(prover, "set_message_sink") and not self.replicated
+        self._claim = None     # global claim of the coming round (device path)
+        self._last_pts = None  # previous round's global points (device path)
+        if self.device_exchange:
+            import torch
+            dev = _device_for(dist, group)
+            self._sink = torch.zeros(SINK_WORDS, dtype=torch.int32, device=dev)
+            self._recv = torch.empty(self.world * SINK_WORDS, dtype=torch.int32, device=dev)
+            self._h_recv = torch.empty(self.world * SINK_WORDS, dtype=torch.int32, pin_memory=True)
+            self._pstream = torch.cuda.ExternalStream(prover.stream_handle(), device=dev)
+            prover.set_message_sink(self._sink)
 
     def _gather_if_needed(self):
         if not self.replicated and self.prover.needs_gather():
@@ -112,21 +141,61 @@ class ShardedSumcheck:
             self.exchange_seconds += ex.seconds
             self.prover.import_gathered(allw.reshape(-1), self.world)
             self.replicated = True
+            if self.device_exchange:
+                self.prover.set_message_sink(None)
+
+    def _device_round(self, d1):
+        import time
+        import torch
+        import torch.distributed as dist
+        t0 = time.perf_counter()
+        torch.cuda.current_stream(self._sink.device).wait_stream(self._pstream)
+        dist.all_gather_into_tensor(self._recv, self._sink, group=self.group)
+        self._h_recv.copy_(self._recv)  # synchronous: the host needs the words now
+        g = self._h_recv.numpy().view(np.uint32).reshape(self.world, SINK_WORDS)
+        raw = np.bitwise_xor.reduce(g[:, :4 * d1], axis=0).reshape(d1, 4).copy()
+        flags = int(g[0, 36])
+        if flags & 2:  # the last call (one evaluation left): words 0-3 are prod_j f_j(r)
+            s = raw[0].copy()
+            raw[:] = 0
+        elif flags & 1:  # p(1) was not computed: complete it from the global claim
+            if self._claim is None:
+                raise RuntimeError("ShardedSumcheck: p(1) skipped without a global claim")
+            raw[1] = self._claim ^ raw[0]
+            s = self._claim.copy()
+        else:
+            s = raw[0] ^ raw[1]
+        self.exchange_seconds += time.perf_counter() - t0
+        self.exchange_rounds += 1
+        return s, raw
 
     def this_round_messages(self):
         self._gather_if_needed()
         s, pts = self.prover.this_round_messages()
         d1 = pts.shape[0]
+        if self.replicated:
+            self._last_pts = None
+            return s, pts
+        if self.device_exchange:
+            s, pts = self._device_round(d1)
+            self._last_pts = pts
+            return s, pts
         flat = np.concatenate([np.asarray(s, np.uint32).reshape(-1), np.asarray(pts, np.uint32).reshape(-1)])
-        if not self.replicated:
-            if self._msg is None:
-                self._msg = WordExchange(flat.size, self.group)
-            t = self._msg.seconds
-            flat = self._msg.xor(flat)
-            self.exchange_seconds += self._msg.seconds - t
-            self.exchange_rounds += 1
+        if self._msg is None:
+            self._msg = WordExchange(flat.size, self.group)
+        t = self._msg.seconds
+        flat = self._msg.xor(flat)
+        self.exchange_seconds += self._msg.seconds - t
+        self.exchange_rounds += 1
         return flat[:4].copy(), flat[4:].reshape(d1, 4).copy()
 
     def move_to_next_round(self, challenge):
         self._gather_if_needed()
         self.prover.move_to_next_round(challenge)
+        # the next round's global claim, computed while its messages kernel runs
+        if self.device_exchange and self._last_pts is not None:
+            from . import evaluate_univariate_given_points
+            self._claim = np.asarray(evaluate_univariate_given_points(challenge, self._last_pts), np.uint32)
+        else:
+            self._claim = None
+        self._last_pts = None

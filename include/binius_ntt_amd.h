@@ -163,6 +163,15 @@ typedef struct bn_sumcheck bn_sumcheck;
  * The host copy is made synchronously. */
 int bn_sumcheck_create(int device, int num_vars, int composition_size, int data_is_transposed,
                        const uint32_t* evals, bn_sumcheck** sc);
+/* bn_sumcheck_create in the reference constructor's two timed phases (sumcheck.cuh:88-124:
+ * start_before_memcpy, start_before_transpose, start_raw): _staged allocates and copies the host
+ * columns (synchronous, the "Memcpy" phase) and leaves compact input untransposed;
+ * bn_sumcheck_prepare runs the device bit-transpose and synchronises (the "Transpose" phase; a
+ * no-op for bitsliced input or a prepared prover). A staged prover used without prepare is
+ * prepared by its first round call. */
+int bn_sumcheck_create_staged(int device, int num_vars, int composition_size, int data_is_transposed,
+                              const uint32_t* evals, bn_sumcheck** sc);
+int bn_sumcheck_prepare(bn_sumcheck* sc);
 /* As above but from device memory already holding the columns (no host copy). The buffer
  * is copied into the prover's own storage unless take_ownership != 0, in which case the
  * prover folds it in place and frees it with hipFree on destroy (so it must come from
@@ -198,6 +207,17 @@ int bn_sumcheck_create_shard_device(int device, int num_vars, int composition_si
  * (composition_size * 128 words), the caller all-gathers them rank-major and every rank
  * imports the concatenation; the prover then continues unsharded. */
 int bn_sumcheck_needs_gather(const bn_sumcheck* sc, int* flag);
+/* Device-resident round exchange (no reference counterpart): every later round-messages kernel also
+ * writes the round's raw point words into d_words (device memory, >= 4*(8+1)+1 words, or NULL to
+ * stop): words 0 .. 4*(composition_size+1)-1 = the kernel's points 0..d (p(1) zero when it was not
+ * computed), word 36 = flags: bit 0 set if p(1) was left out (the caller then has p(1) = claim + p(0)
+ * and sum = claim with the round's claim, which for XOR-combined shards is the global one; clear:
+ * sum = p(0) + p(1)); bit 1 set for the last call (one evaluation left: words 0-3 are the sum,
+ * prod_j f_j(r), and there are no points). The words are written before the posted sequence number, so they are complete
+ * once bn_sumcheck_round_messages has returned; consumers on other streams order themselves after
+ * the prover's stream (bn_sumcheck_stream) to read them. */
+int bn_sumcheck_set_message_sink(bn_sumcheck* sc, void* d_words);
+int bn_sumcheck_stream(const bn_sumcheck* sc, void** stream);
 int bn_sumcheck_export_shard(const bn_sumcheck* sc, uint32_t* out, size_t out_words);
 int bn_sumcheck_import_gathered(bn_sumcheck* sc, const uint32_t* words, size_t n_words, int world);
 int bn_sumcheck_destroy(bn_sumcheck* sc);

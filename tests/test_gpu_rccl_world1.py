@@ -1,8 +1,9 @@
 """RCCL rehearsal on one GPU: the exact process-group call bench.py makes for N > 1
 (`init_process_group("nccl", device_id=cuda:local)`), the device branch of
 `distributed.WordExchange` (pinned host staging, `all_gather_into_tensor` on the GPU, one copy
-back), the max-over-ranks `all_reduce` and a barrier, all over the nccl (= RCCL) backend with world
-size 1. A single GPU cannot hold two RCCL ranks, so this is as far as the multi-GPU data path can
+back), the max-over-ranks `all_reduce` and a barrier, and ShardedSumcheck's device-resident round
+exchange (the prover's message sink gathered directly) against an unsharded transcript, all over
+the nccl (= RCCL) backend with world size 1. A single GPU cannot hold two RCCL ranks, so this is as far as the multi-GPU data path can
 run before the driver's 8-GPU bench; its multi-rank logic is covered by the gloo tests
 (tests/test_distributed.py, tests/test_bench_cli.py)."""
 import os
@@ -35,7 +36,40 @@ SCRIPT = textwrap.dedent("""
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dist.barrier()
     assert t.item() == 1.5 and ex.calls == 6
+
+    # the sharded prover's device-resident exchange (message sink -> all_gather_into_tensor ->
+    # one copy back, p(1) completed from the global claim), forced at world 1, against an
+    # unsharded prover's transcript; and the host-staged path (WordExchange) beside it
+    import json, time
+    import binius_ntt_amd as B
+    n, d = 18, 3
+    rng = np.random.default_rng(1818)
+    ev = rng.integers(0, 2**32, size=d * (4 << n), dtype=np.uint64).astype(np.uint32)
+    ch = rng.integers(0, 2**32, size=(n, 4), dtype=np.uint64).astype(np.uint32)
+    def transcript(sc):
+        out = []
+        for r in range(n + 1):
+            s, p = sc.this_round_messages()
+            out.append((s.copy(), p.copy()))
+            if r < n:
+                sc.move_to_next_round(ch[r])
+        return out
+    ref = B.Sumcheck(n, d, True, ev)
+    want = transcript(ref)
+    ref.close()
+    stats = {}
+    for mode in ("device", "host"):
+        pr = B.Sumcheck(n, d, True, ev)
+        sc = D.ShardedSumcheck(pr, device_exchange=(mode == "device"), exchange_at_world1=True)
+        assert sc.device_exchange == (mode == "device")
+        got = transcript(sc)
+        for r, ((s1, p1), (s2, p2)) in enumerate(zip(got, want)):
+            assert np.array_equal(s1, s2) and np.array_equal(p1, p2), (mode, r)
+        assert sc.exchange_rounds == n + 1
+        stats[mode + "_exchange_ms_per_round"] = sc.exchange_seconds * 1e3 / sc.exchange_rounds
+        pr.close()
     dist.destroy_process_group()
+    print("EXCHANGE " + json.dumps(dict(stats, n=n, d=d, world=1, backend="nccl")))
     print("rccl world1 ok")
 """)
 
@@ -51,3 +85,6 @@ def test_rccl_process_group_and_word_exchange_world1():
     r = subprocess.run([sys.executable, "-c", SCRIPT, ROOT], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "rccl world1 ok" in r.stdout
+    for line in r.stdout.splitlines():
+        if line.startswith("EXCHANGE "):
+            print(line)  # per-round exchange cost of both paths (pytest -s shows it)

@@ -3,9 +3,8 @@
 // the same configurations (NUM_VARS 20/24/28 x COMPOSITION_SIZE 2/3/4), run counts (10/5/2 after
 // one warm-up sample), compact input from a host std::vector (DATA_IS_TRANSPOSED = false) and the
 // same three phases per sample:
-//   Memcpy    = constructor: host -> HBM copy (pageable std::vector) and, in this build, the device
-//               bit-transpose as well (bn_sumcheck_create does both, then synchronises)
-//   Transpose = 0 (folded into Memcpy, see above)
+//   Memcpy    = constructor, bn_sumcheck_create_staged: host -> HBM copy (pageable std::vector)
+//   Transpose = constructor, bn_sumcheck_prepare: the device compact -> bitsliced transpose
 //   Raw       = every round's this_round_messages + move_to_next_round, then the last messages
 // Output: the reference's text lines per configuration, then one JSON line with every result.
 // Build + run: tools/run_benchmark_sumcheck.sh
