@@ -99,9 +99,9 @@ class ShardedSumcheck:
 
     Exchange paths for the per-round (sum, points) words:
       * device (default on an nccl group with a HIP prover): the prover's messages kernel also writes
-        its raw partial points into a preallocated device sink (bn_sumcheck_set_message_sink), the
-        current stream waits for the prover's stream, `all_gather_into_tensor` reads the sink
-        directly and one copy brings the world x 40 words back; the partial points are XOR-ed and
+        its raw partial points into a preallocated device sink (bn_sumcheck_set_message_sink),
+        `all_gather_into_tensor` reads the sink directly and one copy brings the world x 40 words
+        back; the partial points are XOR-ed and
         p(1), sum are completed from the GLOBAL claim (p(1) = claim + p(0), sum = claim, the claim
         being the previous round's global points interpolated at its challenge) — so no
         numpy -> pinned -> H2D hop per round;
@@ -130,7 +130,6 @@ class ShardedSumcheck:
             self._sink = torch.zeros(SINK_WORDS, dtype=torch.int32, device=dev)
             self._recv = torch.empty(self.world * SINK_WORDS, dtype=torch.int32, device=dev)
             self._h_recv = torch.empty(self.world * SINK_WORDS, dtype=torch.int32, pin_memory=True)
-            self._pstream = torch.cuda.ExternalStream(prover.stream_handle(), device=dev)
             prover.set_message_sink(self._sink)
 
     def _gather_if_needed(self):
@@ -149,7 +148,10 @@ class ShardedSumcheck:
         import torch
         import torch.distributed as dist
         t0 = time.perf_counter()
-        torch.cuda.current_stream(self._sink.device).wait_stream(self._pstream)
+        # no stream wait: the prover's this_round_messages has already seen the round's posted
+        # sequence number, which the posting workgroup releases at system scope after writing the
+        # sink words, and the collective's kernel is dispatched after that (with the dispatch's
+        # acquire), so it reads the complete words
         dist.all_gather_into_tensor(self._recv, self._sink, group=self.group)
         self._h_recv.copy_(self._recv)  # synchronous: the host needs the words now
         g = self._h_recv.numpy().view(np.uint32).reshape(self.world, SINK_WORDS)
