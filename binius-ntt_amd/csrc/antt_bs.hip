@@ -33,6 +33,7 @@
 
 #include "antt_bs.hpp"
 #include "bitsliced.hpp"
+#include "quad_mul.hpp"
 
 namespace bn {
 
@@ -426,6 +427,276 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 }
 
 // ------------------------------------------------------------------------------------
+// Lane-split passes (small launches). A pass of T tiles runs 4T waves above; below two tiles per CU
+// (one 2^20 transform: 256 tiles, one wave per SIMD) a lone wave issues at half the rate of two
+// (DESIGN.md section 5.1). Here each GF(2^32) product of a block pair is split over three waves by
+// the tower's top Karatsuba level (v = v0 + v1 X, w = w0 + w1 X over GF(2^16)):
+//   wave term 0: z0 = w0 v0,  term 1: z2 = w1 v1,  term 2: z1 = (w0 + w1)(v0 + v1)   (bsm4, 316 gates)
+//   then term 0 forms the low half  w v|lo = z0 + z2                 and updates u, v words 0..15,
+//        term 1 the high half       w v|hi = z1 + z0 + z2 + alpha(z2) and words 16..31
+//   (disjoint words: the read-modify-writes of u need no ordering among the waves),
+// so a work-group of 12 waves (4 limbs x 3 terms, three waves per SIMD) runs each stage's product at a
+// third of the per-wave instructions. Two work-group barriers per stage: the partials are complete
+// before they are combined, and a stage's u, v words are written before the next stage reads them
+// (and before a partial slot is overwritten). Same tiles, tables, HBM layouts and results as
+// antt_bs_pass.
+// ------------------------------------------------------------------------------------
+constexpr int kSplitNT = 768;           // 12 waves
+constexpr int kZStride = 20;            // LDS words per lane of a partial product (16 + 4: bank spread)
+constexpr int kZWave = 64 * kZStride;   // one wave's partial products
+static size_t split_lds_bytes() {
+	return ((size_t)4 * kPlane + (size_t)12 * kZWave + (size_t)kMaxStages) * sizeof(uint32_t);
+}
+
+template <int ROLE>
+__global__ __launch_bounds__(kSplitNT, 1) void antt_bs3_pass(BsParams P) {
+	extern __shared__ uint32_t lds[];
+	constexpr int L = 4;
+	constexpr bool IN_COMPACT = ROLE == ROLE_FIRST || ROLE == ROLE_SINGLE;
+	constexpr bool LAST = ROLE == ROLE_LAST || ROLE == ROLE_SINGLE;
+	const BsPass& ps = P.p;
+	const int tid = threadIdx.x;
+	const int w = tid >> 6, lane = tid & 63;
+	const int l = w & 3, term = w >> 2;  // limb plane, Karatsuba term
+	uint32_t* const zb = lds + 4 * kPlane;        // [limb][term][lane][kZStride]
+	uint32_t* const cu_w = zb + 12 * kZWave;      // workgroup-uniform twiddle part per stage
+	const size_t n = (size_t)1 << P.log_h;
+	auto tile_off = [&](int q) -> size_t {
+		size_t off = 0;
+#pragma unroll
+		for (int m = 0; m < kBlkBits; m++) off |= (size_t)((q >> m) & 1) << ps.bb[m];
+		return off;
+	};
+	const size_t tile = blockIdx.x;
+	const size_t outer = tile & (((size_t)1 << ps.n_outer) - 1);
+	const size_t rest = tile >> ps.n_outer;
+	const int coset = (int)(rest & ((1u << P.log_rate) - 1));
+	const size_t batch = rest >> P.log_rate;
+	size_t ooff = 0;
+	for (int m = 0; m < ps.n_outer; m++) ooff |= ((outer >> m) & 1) << ps.ob[m];
+	uint32_t* dst = P.dst + (((batch << P.log_rate) + (size_t)coset) * n) * L;
+	const uint32_t* src = IN_COMPACT ? (P.src + batch * n * L) : dst;
+
+	if (tid < ps.k) {
+		uint32_t c = 0;
+		for (int m = 0; m < ps.n_outer; m++) c ^= ps.two[tid][m] & (0u - (uint32_t)((outer >> m) & 1));
+		for (int b = 0; b < P.log_rate; b++) c ^= ps.twc[tid][b] & (0u - (uint32_t)((coset >> b) & 1));
+		cu_w[tid] = c;
+	}
+	// ---- tile into LDS: 4096 pieces of 16 bytes, at most 6 per thread, all loads in flight at once
+	constexpr int kRounds = (kTileBlocks * 8 * L + kSplitNT - 1) / kSplitNT;
+	uint4 g[kRounds];
+#pragma unroll
+	for (int r = 0; r < kRounds; r++) {
+		const int u = tid + r * kSplitNT;
+		if (u < kTileBlocks * 8 * L) {
+			if (IN_COMPACT) {
+				const int q = u / (8 * L), j = u % (8 * L);
+				g[r] = ld_stream(src + (ooff | tile_off(q)) * L + 4 * j);
+			} else {
+				const int pl = u >> 10, rr = u & 1023, q = rr >> 3, j = rr & 7;  // plane, block, 16-B chunk
+				g[r] = ld_stream(src + (ooff | tile_off(q)) * L + 32 * pl + 4 * j);
+			}
+		}
+	}
+#pragma unroll
+	for (int r = 0; r < kRounds; r++) {
+		const int u = tid + r * kSplitNT;
+		if (u < kTileBlocks * 8 * L) {
+			if (IN_COMPACT) {
+				const int q = u / (8 * L), j = u % (8 * L);
+				const uint32_t wd[4] = {g[r].x, g[r].y, g[r].z, g[r].w};
+#pragma unroll
+				for (int c = 0; c < 4; c++) {
+					const int word = 4 * j + c;
+					lds[(word % L) * kPlane + q * kLimbStride + word / L] = wd[c];
+				}
+			} else {
+				const int pl = u >> 10, rr = u & 1023, q = rr >> 3, j = rr & 7;
+				*(uint4*)(lds + pl * kPlane + q * kLimbStride + 4 * j) = g[r];
+			}
+		}
+	}
+	__syncthreads();
+	if (IN_COMPACT) {
+		// 512 per-(block, limb) 32x32 transposes, one per thread
+		for (int g = tid; g < kTileBlocks * L; g += kSplitNT) {
+			uint32_t* x = lds + (g >> 7) * kPlane + (g & 127) * kLimbStride;
+			uint32_t r[32];
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) *(uint4*)(r + i) = *(const uint4*)(x + i);
+			transpose32(r);
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) *(uint4*)(x + i) = *(const uint4*)(r + i);
+		}
+		__syncthreads();
+	}
+	uint32_t* const plane = lds + l * kPlane;
+	uint32_t* const zme = zb + (l * 3 + term) * kZWave + lane * kZStride;
+	const uint32_t* const z0p = zb + (l * 3 + 0) * kZWave + lane * kZStride;
+	const uint32_t* const z2p = zb + (l * 3 + 1) * kZWave + lane * kZStride;
+	const uint32_t* const z1p = zb + (l * 3 + 2) * kZWave + lane * kZStride;
+	// this wave's term of the product of the 32-word operand X (given as its two halves) and the
+	// twiddle half words W (16 words: bit i of each bit-lane's 16-bit twiddle half in word i), into
+	// the LDS partial slot
+	auto term_product = [&](const uint32_t* X0, const uint32_t* X1, const uint32_t* wv) {
+		uint32_t x[16], z[16];
+#pragma unroll
+		for (int i = 0; i < 16; i++) x[i] = term == 0 ? X0[i] : term == 1 ? X1[i] : X0[i] ^ X1[i];
+		__builtin_amdgcn_sched_barrier(0);
+		bsm4_mul(x, wv, z);
+		__builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+		for (int i = 0; i < 16; i += 4) *(uint4*)(zme + i) = make_uint4(z[i], z[i + 1], z[i + 2], z[i + 3]);
+	};
+	// half `term` (0: words 0..15, 1: 16..31) of the product w v from the three partials:
+	// lo = z0 + z2, hi = z1 + z0 + z2 + alpha(z2)
+	auto product_half = [&](uint32_t* p) {
+		uint32_t c[16];
+#pragma unroll
+		for (int i = 0; i < 16; i += 4) {
+			*(uint4*)(p + i) = *(const uint4*)(z0p + i);
+			*(uint4*)(c + i) = *(const uint4*)(z2p + i);
+		}
+		if (term == 0) {
+#pragma unroll
+			for (int i = 0; i < 16; i++) p[i] ^= c[i];
+		} else {
+			uint32_t e[16], al[16];
+#pragma unroll
+			for (int i = 0; i < 16; i += 4) *(uint4*)(e + i) = *(const uint4*)(z1p + i);
+			quad::bs_alpha<4>(c, al);
+#pragma unroll
+			for (int i = 0; i < 16; i++) p[i] = BN_XOR3(p[i], c[i], e[i]) ^ al[i];
+		}
+	};
+	// the 16-bit twiddle half this wave's term multiplies by, as words (bit i of every bit-lane's
+	// half in word i): term 0 the low half, 1 the high half, 2 their sum
+	auto half_of = [&](uint32_t tw) -> uint32_t {
+		return term == 0 ? (tw & 0xFFFFu) : term == 1 ? (tw >> 16) : ((tw ^ (tw >> 16)) & 0xFFFFu);
+	};
+	auto tile_tw = [&](int j, int q) -> uint32_t {
+		uint32_t tw = 0;
+#pragma unroll
+		for (int m = 0; m < kBlkBits; m++) tw ^= ps.twt[j][m] & (uint32_t)__builtin_amdgcn_sbfe(q, m, 1);
+		return tw;
+	};
+
+	// ---- tile-bit stages: lane = block pair of limb l, as antt_bs_pass
+	const int jlow = max(LAST ? 5 : 0, ps.stop_j);
+	for (int j = ps.k - 1; j >= jlow; j--) {
+		const int m = ps.stage_m[j];
+		const int qu = ((lane >> m) << (m + 1)) | (lane & ((1 << m) - 1));
+		const int qv = qu | (1 << m);
+		uint32_t* pu = plane + qu * kLimbStride;
+		uint32_t* pv = plane + qv * kLimbStride;
+		{
+			const uint32_t wt = half_of(cu_w[j] ^ tile_tw(j, qu));
+			uint32_t W[16];
+#pragma unroll
+			for (int i = 0; i < 16; i++) W[i] = (uint32_t)__builtin_amdgcn_sbfe(wt, i, 1);
+			term_product(pv, pv + 16, W);
+		}
+		__syncthreads();
+		if (term < 2) {
+			uint32_t pr[16];
+			product_half(pr);
+			const int o = 16 * term;
+#pragma unroll
+			for (int i = 0; i < 16; i += 4) {
+				uint4 uu = *(const uint4*)(pu + o + i);
+				const uint4 vv = *(const uint4*)(pv + o + i);
+				uu.x ^= pr[i], uu.y ^= pr[i + 1], uu.z ^= pr[i + 2], uu.w ^= pr[i + 3];
+				*(uint4*)(pu + o + i) = uu;
+				*(uint4*)(pv + o + i) = make_uint4(vv.x ^ uu.x, vv.y ^ uu.y, vv.z ^ uu.z, vv.w ^ uu.w);
+			}
+		}
+		__syncthreads();
+	}
+
+	if (LAST) {
+		// ---- stages 4..0 inside the words (antt_bs_pass's packing: lane owns blocks qa = lane and
+		// qb = lane + 64 of limb l; A's v-lanes move onto the u positions, B's stay)
+		const int qa = lane, qb = qa | (kTileBlocks / 2);
+		uint32_t* pa = plane + qa * kLimbStride;
+		uint32_t* pb = plane + qb * kLimbStride;
+		for (int s = 4; s >= ps.stop_j; s--) {
+			const uint32_t d = vgpr(1u << s);
+			const uint32_t um = vgpr(~lane_mask(s));
+			{
+				const uint32_t cb = cu_w[s] ^ tile_tw(s, qb);
+				uint32_t T[32], W[16];
+#pragma unroll
+				for (int i = 0; i < 32; i += 4) {
+					const uint4 a = *(const uint4*)(pa + i), b = *(const uint4*)(pb + i);
+					T[i] = __builtin_amdgcn_bitop3_b32(a.x >> d, b.x, um, 0xe4);
+					T[i + 1] = __builtin_amdgcn_bitop3_b32(a.y >> d, b.y, um, 0xe4);
+					T[i + 2] = __builtin_amdgcn_bitop3_b32(a.z >> d, b.z, um, 0xe4);
+					T[i + 3] = __builtin_amdgcn_bitop3_b32(a.w >> d, b.w, um, 0xe4);
+				}
+				// twiddle words: the bit-lane pattern plus the block part (antt_bs_pass), this term's half
+#pragma unroll
+				for (int i = 0; i < 16; i++) {
+					const uint32_t lo = ps.pat[s][i] ^ (uint32_t)__builtin_amdgcn_sbfe(cb, i, 1);
+					const uint32_t hi = ps.pat[s][16 + i] ^ (uint32_t)__builtin_amdgcn_sbfe(cb, 16 + i, 1);
+					W[i] = term == 0 ? lo : term == 1 ? hi : lo ^ hi;
+				}
+				term_product(T, T + 16, W);
+			}
+			__syncthreads();
+			if (term < 2) {
+				uint32_t pr[16];
+				product_half(pr);
+				const int o = 16 * term;
+#pragma unroll
+				for (int i = 0; i < 16; i += 4) {
+					uint32_t A[4], Bv[4];
+					*(uint4*)A = *(const uint4*)(pa + o + i);
+					*(uint4*)Bv = *(const uint4*)(pb + o + i);
+#pragma unroll
+					for (int c = 0; c < 4; c++) {
+						const uint32_t a = __builtin_amdgcn_bitop3_b32(pr[i + c], um, A[c], 0x6a);
+						const uint32_t b = __builtin_amdgcn_bitop3_b32(pr[i + c] >> d, um, Bv[c], 0x6a);
+						A[c] = __builtin_amdgcn_bitop3_b32(a << d, um, a, 0x9a);
+						Bv[c] = __builtin_amdgcn_bitop3_b32(b << d, um, b, 0x9a);
+					}
+					*(uint4*)(pa + o + i) = *(const uint4*)A;
+					*(uint4*)(pb + o + i) = *(const uint4*)Bv;
+				}
+			}
+			__syncthreads();
+		}
+		// back to compact words: 512 block transposes, one per thread
+		for (int g = tid; g < kTileBlocks * L; g += kSplitNT) {
+			uint32_t* x = lds + (g >> 7) * kPlane + (g & 127) * kLimbStride;
+			uint32_t r[32];
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) *(uint4*)(r + i) = *(const uint4*)(x + i);
+			transpose32(r);
+#pragma unroll
+			for (int i = 0; i < 32; i += 4) *(uint4*)(x + i) = *(const uint4*)(r + i);
+		}
+		__syncthreads();
+		for (int u = tid; u < kTileBlocks * 8 * L; u += kSplitNT) {
+			const int q = u / (8 * L), j = u % (8 * L);
+			uint32_t wd[4];
+#pragma unroll
+			for (int c = 0; c < 4; c++) {
+				const int word = 4 * j + c;
+				wd[c] = lds[(word % L) * kPlane + q * kLimbStride + word / L];
+			}
+			if (!(BS_DBG(P) & 2)) st_stream(dst + (ooff | tile_off(q)) * L + 4 * j, make_uint4(wd[0], wd[1], wd[2], wd[3]));
+		}
+	} else {
+		for (int u = tid; u < kTileBlocks * 8 * L; u += kSplitNT) {
+			const int pl = u >> 10, r = u & 1023, q = r >> 3, j = r & 7;
+			const uint4 g = *(const uint4*)(lds + pl * kPlane + q * kLimbStride + 4 * j);
+			if (!(BS_DBG(P) & 2)) st_stream(dst + (ooff | tile_off(q)) * L + 32 * pl + 4 * j, g);
+		}
+	}
+}
+
+// ------------------------------------------------------------------------------------
 // host: pass planning
 // ------------------------------------------------------------------------------------
 static std::vector<BsPass> plan_passes(const bn_antt_plan* plan) {
@@ -539,6 +810,15 @@ static const void* kernel_for(int L, int role, int fmax, bool pf) {
 	return fmax <= 8 ? kernel_for_f<1, 8>(role, pf) : kernel_for_f<1, 32>(role, pf);
 }
 
+static const void* split_kernel_for(int role) {
+	switch (role) {
+		case ROLE_FIRST: return (const void*)antt_bs3_pass<ROLE_FIRST>;
+		case ROLE_MID: return (const void*)antt_bs3_pass<ROLE_MID>;
+		case ROLE_LAST: return (const void*)antt_bs3_pass<ROLE_LAST>;
+		default: return (const void*)antt_bs3_pass<ROLE_SINGLE>;
+	}
+}
+
 int pass_fmax(const BsPass& p) {
 	int f = 8;
 	for (int j = 0; j < p.k; j++) f = std::max(f, p.field[j]);
@@ -559,6 +839,8 @@ int bs_prepare(bn_antt_plan* plan) {
 				for (int pf = 0; pf < 2; pf++)
 					BN_HIP(hipFuncSetAttribute(kernel_for(L, role, f, pf != 0), hipFuncAttributeMaxDynamicSharedMemorySize,
 					                           (int)lds_bytes(L)));
+	for (int role = 0; role < 4; role++)
+		BN_HIP(hipFuncSetAttribute(split_kernel_for(role), hipFuncAttributeMaxDynamicSharedMemorySize, (int)split_lds_bytes()));
 	int rc = rr_prepare(plan);
 	if (rc != BN_OK) return rc;
 	int cus = 0;
@@ -580,7 +862,7 @@ const BsPass* bs_passes(bn_antt_plan* plan, size_t* n_passes) {
 }
 
 struct BsDevKnobs {
-	int pf_mode = 0, dbg = 0, stop_stage = -1;
+	int pf_mode = 0, dbg = 0, stop_stage = -1, split = -1;
 	bool persist = true, trace = false;
 	size_t max_passes = ~(size_t)0;
 };
@@ -597,9 +879,18 @@ static BsDevKnobs dev_knobs() {
 	if (const char* e = getenv("BN_PERSIST")) k.persist = atoi(e) != 0;
 	if (const char* e = getenv("BN_DEBUG_FLAGS")) k.dbg = atoi(e);
 	if (const char* e = getenv("BN_DEBUG_STOP_STAGE")) k.stop_stage = atoi(e);
+	if (const char* e = getenv("BN_SPLIT")) k.split = atoi(e);  // 0: never lane-split, 1: always
 	k.trace = getenv("BN_TRACE") != nullptr;
 #endif
 	return k;
+}
+
+// GF(2^16/32) LDS-tile passes of fewer tiles than two per CU (one 2^20 transform) run lane-split
+// (antt_bs3_pass: three waves per product, three waves per SIMD instead of one)
+static bool use_split(const bn_antt_plan* plan, const BsPass& pass, size_t ntiles, const BsDevKnobs& kn) {
+	if (plan->limbs != 4 || pass_fmax(pass) <= 8) return false;
+	if (kn.split >= 0) return kn.split != 0;
+	return ntiles < (size_t)2 * (size_t)plan->num_cus;
 }
 
 static int launch_one(bn_antt_plan* plan, const BsPass& pass, int i, const uint32_t* d_in, uint32_t* d_out,
@@ -617,6 +908,15 @@ static int launch_one(bn_antt_plan* plan, const BsPass& pass, int i, const uint3
 	prm.p = pass;
 	prm.p.stop_j = kn.stop_stage < 0 ? 0 : std::max(0, std::min(prm.p.k, kn.stop_stage - prm.p.lo));
 	const size_t ntiles = (batch << plan->log_rate) << pass.n_outer;
+	if (use_split(plan, pass, ntiles, kn)) {
+		prm.ntiles = ntiles;
+		prm.trace = nullptr;
+		int rc = timing_begin(plan, i, st);
+		if (rc != BN_OK) return rc;
+		void* args[] = {&prm};
+		BN_HIP(hipLaunchKernel(split_kernel_for(pass.role), dim3((unsigned)ntiles), dim3(kSplitNT), args, split_lds_bytes(), st));
+		return timing_end(plan, i, st);
+	}
 	// two 74-KB tiles per CU: a persistent grid of two workgroups per CU walks all tiles
 	const int fmax = pass_fmax(pass);
 	const bool pf = kn.persist && (kn.pf_mode == 2 || (kn.pf_mode == 1 && fmax <= 8));
@@ -661,6 +961,8 @@ const void* bs_pass_kernel(bn_antt_plan* plan, int i) {
 	if (plan->variant == 4 || (plan->variant == 5 && fmax <= 8)) return rr_pass_kernel(plan, pass);
 	if (plan->variant != 1 && plan->variant != 5) return nullptr;
 	const BsDevKnobs kn = dev_knobs();
+	const size_t ntiles = ((size_t)1 << plan->log_rate) << pass.n_outer;  // one transform (bench / profiles)
+	if (use_split(plan, pass, ntiles, kn)) return split_kernel_for(pass.role);
 	const bool pf = kn.persist && (kn.pf_mode == 2 || (kn.pf_mode == 1 && fmax <= 8));
 	return kernel_for(plan->limbs, pass.role, fmax, pf);
 }
