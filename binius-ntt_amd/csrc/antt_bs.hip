@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "antt_bs.hpp"
@@ -429,24 +430,18 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 // ------------------------------------------------------------------------------------
 // Lane-split passes (small launches). A pass of T tiles runs 4T waves above; below two tiles per CU
 // (one 2^20 transform: 256 tiles, one wave per SIMD) a lone wave issues at half the rate of two
-// (DESIGN.md section 5.1). Here each GF(2^32) product of a block pair is split over three waves by
-// the tower's top Karatsuba level (v = v0 + v1 X, w = w0 + w1 X over GF(2^16)):
-//   wave term 0: z0 = w0 v0,  term 1: z2 = w1 v1,  term 2: z1 = (w0 + w1)(v0 + v1)   (bsm4, 316 gates)
-//   then term 0 forms the low half  w v|lo = z0 + z2                 and updates u, v words 0..15,
-//        term 1 the high half       w v|hi = z1 + z0 + z2 + alpha(z2) and words 16..31
-//   (disjoint words: the read-modify-writes of u need no ordering among the waves),
-// so a work-group of 12 waves (4 limbs x 3 terms, three waves per SIMD) runs each stage's product at a
-// third of the per-wave instructions. Two work-group barriers per stage: the partials are complete
-// before they are combined, and a stage's u, v words are written before the next stage reads them
-// (and before a partial slot is overwritten). Same tiles, tables, HBM layouts and results as
+// (DESIGN.md section 5.1). Here each GF(2^32) product of a block pair is split over two waves by the
+// tower's top level (v = v0 + v1 X, w = w0 + w1 X over GF(2^16), X^2 = alpha X + 1):
+//   wave half 0: (w v)|lo = v0 w0 + v1 w1                 -> words 0..15 of u and v
+//   wave half 1: (w v)|hi = v0 w1 + v1 (w0 + alpha w1)    -> words 16..31
+// two GF(2^16) products per wave (bsm4, 316 gates: 1264 for the pair against one 1022-gate bsm5)
+// and no partial products to exchange. The tile is double-buffered in LDS (a stage reads one copy
+// and writes the other), so one work-group barrier per stage orders every access. A work-group is
+// 8 waves (4 limbs x 2 halves): two waves per SIMD. Same tiles, tables, HBM layouts and results as
 // antt_bs_pass.
 // ------------------------------------------------------------------------------------
-constexpr int kSplitNT = 768;           // 12 waves
-constexpr int kZStride = 20;            // LDS words per lane of a partial product (16 + 4: bank spread)
-constexpr int kZWave = 64 * kZStride;   // one wave's partial products
-static size_t split_lds_bytes() {
-	return ((size_t)4 * kPlane + (size_t)12 * kZWave + (size_t)kMaxStages) * sizeof(uint32_t);
-}
+constexpr int kSplitNT = 512;  // 8 waves
+static size_t split_lds_bytes() { return ((size_t)8 * kPlane + (size_t)kMaxStages) * sizeof(uint32_t); }
 
 template <int ROLE>
 __global__ __launch_bounds__(kSplitNT, 1) void antt_bs3_pass(BsParams P) {
@@ -456,10 +451,9 @@ __global__ __launch_bounds__(kSplitNT, 1) void antt_bs3_pass(BsParams P) {
 	constexpr bool LAST = ROLE == ROLE_LAST || ROLE == ROLE_SINGLE;
 	const BsPass& ps = P.p;
 	const int tid = threadIdx.x;
-	const int w = tid >> 6, lane = tid & 63;
-	const int l = w & 3, term = w >> 2;  // limb plane, Karatsuba term
-	uint32_t* const zb = lds + 4 * kPlane;        // [limb][term][lane][kZStride]
-	uint32_t* const cu_w = zb + 12 * kZWave;      // workgroup-uniform twiddle part per stage
+	const int w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+	const int l = w & 3, half = w >> 2;  // limb plane, product half
+	uint32_t* const cu_w = lds + 8 * kPlane;  // workgroup-uniform twiddle part per stage
 	const size_t n = (size_t)1 << P.log_h;
 	auto tile_off = [&](int q) -> size_t {
 		size_t off = 0;
@@ -483,97 +477,90 @@ __global__ __launch_bounds__(kSplitNT, 1) void antt_bs3_pass(BsParams P) {
 		for (int b = 0; b < P.log_rate; b++) c ^= ps.twc[tid][b] & (0u - (uint32_t)((coset >> b) & 1));
 		cu_w[tid] = c;
 	}
-	// ---- tile into LDS: 4096 pieces of 16 bytes, at most 6 per thread, all loads in flight at once
+	// ---- tile into LDS copy 0: 4096 pieces of 16 bytes, 8 per thread, all loads in flight at once
 	constexpr int kRounds = (kTileBlocks * 8 * L + kSplitNT - 1) / kSplitNT;
 	uint4 g[kRounds];
 #pragma unroll
 	for (int r = 0; r < kRounds; r++) {
 		const int u = tid + r * kSplitNT;
-		if (u < kTileBlocks * 8 * L) {
-			if (IN_COMPACT) {
-				const int q = u / (8 * L), j = u % (8 * L);
-				g[r] = ld_stream(src + (ooff | tile_off(q)) * L + 4 * j);
-			} else {
-				const int pl = u >> 10, rr = u & 1023, q = rr >> 3, j = rr & 7;  // plane, block, 16-B chunk
-				g[r] = ld_stream(src + (ooff | tile_off(q)) * L + 32 * pl + 4 * j);
-			}
+		if (IN_COMPACT) {
+			const int q = u / (8 * L), j = u % (8 * L);
+			g[r] = ld_stream(src + (ooff | tile_off(q)) * L + 4 * j);
+		} else {
+			const int pl = u >> 10, rr = u & 1023, q = rr >> 3, j = rr & 7;  // plane, block, 16-B chunk
+			g[r] = ld_stream(src + (ooff | tile_off(q)) * L + 32 * pl + 4 * j);
 		}
 	}
 #pragma unroll
 	for (int r = 0; r < kRounds; r++) {
 		const int u = tid + r * kSplitNT;
-		if (u < kTileBlocks * 8 * L) {
-			if (IN_COMPACT) {
-				const int q = u / (8 * L), j = u % (8 * L);
-				const uint32_t wd[4] = {g[r].x, g[r].y, g[r].z, g[r].w};
+		if (IN_COMPACT) {
+			const int q = u / (8 * L), j = u % (8 * L);
+			const uint32_t wd[4] = {g[r].x, g[r].y, g[r].z, g[r].w};
 #pragma unroll
-				for (int c = 0; c < 4; c++) {
-					const int word = 4 * j + c;
-					lds[(word % L) * kPlane + q * kLimbStride + word / L] = wd[c];
-				}
-			} else {
-				const int pl = u >> 10, rr = u & 1023, q = rr >> 3, j = rr & 7;
-				*(uint4*)(lds + pl * kPlane + q * kLimbStride + 4 * j) = g[r];
+			for (int c = 0; c < 4; c++) {
+				const int word = 4 * j + c;
+				lds[(word % L) * kPlane + q * kLimbStride + word / L] = wd[c];
 			}
+		} else {
+			const int pl = u >> 10, rr = u & 1023, q = rr >> 3, j = rr & 7;
+			*(uint4*)(lds + pl * kPlane + q * kLimbStride + 4 * j) = g[r];
 		}
 	}
 	__syncthreads();
-	if (IN_COMPACT) {
+	auto transpose_blocks = [&](uint32_t* base) {
 		// 512 per-(block, limb) 32x32 transposes, one per thread
-		for (int g = tid; g < kTileBlocks * L; g += kSplitNT) {
-			uint32_t* x = lds + (g >> 7) * kPlane + (g & 127) * kLimbStride;
-			uint32_t r[32];
+		uint32_t* x = base + (tid >> 7) * kPlane + (tid & 127) * kLimbStride;
+		uint32_t r[32];
 #pragma unroll
-			for (int i = 0; i < 32; i += 4) *(uint4*)(r + i) = *(const uint4*)(x + i);
-			transpose32(r);
+		for (int i = 0; i < 32; i += 4) *(uint4*)(r + i) = *(const uint4*)(x + i);
+		transpose32(r);
 #pragma unroll
-			for (int i = 0; i < 32; i += 4) *(uint4*)(x + i) = *(const uint4*)(r + i);
-		}
+		for (int i = 0; i < 32; i += 4) *(uint4*)(x + i) = *(const uint4*)(r + i);
+	};
+	if (IN_COMPACT) {
+		transpose_blocks(lds);
 		__syncthreads();
 	}
-	uint32_t* const plane = lds + l * kPlane;
-	uint32_t* const zme = zb + (l * 3 + term) * kZWave + lane * kZStride;
-	const uint32_t* const z0p = zb + (l * 3 + 0) * kZWave + lane * kZStride;
-	const uint32_t* const z2p = zb + (l * 3 + 1) * kZWave + lane * kZStride;
-	const uint32_t* const z1p = zb + (l * 3 + 2) * kZWave + lane * kZStride;
-	// this wave's term of the product of the 32-word operand X (given as its two halves) and the
-	// twiddle half words W (16 words: bit i of each bit-lane's 16-bit twiddle half in word i), into
-	// the LDS partial slot
-	auto term_product = [&](const uint32_t* X0, const uint32_t* X1, const uint32_t* wv) {
-		uint32_t x[16], z[16];
-#pragma unroll
-		for (int i = 0; i < 16; i++) x[i] = term == 0 ? X0[i] : term == 1 ? X1[i] : X0[i] ^ X1[i];
-		__builtin_amdgcn_sched_barrier(0);
-		bsm4_mul(x, wv, z);
-		__builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-		for (int i = 0; i < 16; i += 4) *(uint4*)(zme + i) = make_uint4(z[i], z[i + 1], z[i + 2], z[i + 3]);
-	};
-	// half `term` (0: words 0..15, 1: 16..31) of the product w v from the three partials:
-	// lo = z0 + z2, hi = z1 + z0 + z2 + alpha(z2)
-	auto product_half = [&](uint32_t* p) {
-		uint32_t c[16];
-#pragma unroll
-		for (int i = 0; i < 16; i += 4) {
-			*(uint4*)(p + i) = *(const uint4*)(z0p + i);
-			*(uint4*)(c + i) = *(const uint4*)(z2p + i);
+	// the stages, instantiated per product half H (its words o = 16 H index register arrays, so they
+	// must be compile-time constants); returns the LDS copy holding the tile afterwards
+	auto stages = [&](auto hc) -> int {
+	constexpr int H = decltype(hc)::value;
+	constexpr int o = 16 * H;
+	int cur = 0;
+	// this wave's half of the product w v: V the 32 operand words, W0 / W1 the twiddle's low / high
+	// halves as words (bit i of every bit-lane's 16-bit half in word i). Twiddles of a sub-field
+	// (the stage's `field`, wave-uniform) leave W1 zero: half h is then V's half h times W0 alone
+	auto half_product = [&](int field, const uint32_t* V, const uint32_t* W0, const uint32_t* W1, uint32_t* p) {
+		if (field <= 8) {
+			__builtin_amdgcn_sched_barrier(0);
+			bsm3_mul(V + o, W0, p);
+			bsm3_mul(V + o + 8, W0, p + 8);
+			__builtin_amdgcn_sched_barrier(0);
+			return;
 		}
-		if (term == 0) {
+		if (field <= 16) {
+			__builtin_amdgcn_sched_barrier(0);
+			bsm4_mul(V + o, W0, p);
+			__builtin_amdgcn_sched_barrier(0);
+			return;
+		}
+		uint32_t a[16], b[16], z[16];
+		if (H == 0) {
 #pragma unroll
-			for (int i = 0; i < 16; i++) p[i] ^= c[i];
+			for (int i = 0; i < 16; i++) a[i] = W0[i], b[i] = W1[i];
 		} else {
-			uint32_t e[16], al[16];
+			uint32_t al[16];
+			quad::bs_alpha<4>(W1, al);
 #pragma unroll
-			for (int i = 0; i < 16; i += 4) *(uint4*)(e + i) = *(const uint4*)(z1p + i);
-			quad::bs_alpha<4>(c, al);
-#pragma unroll
-			for (int i = 0; i < 16; i++) p[i] = BN_XOR3(p[i], c[i], e[i]) ^ al[i];
+			for (int i = 0; i < 16; i++) a[i] = W1[i], b[i] = W0[i] ^ al[i];
 		}
-	};
-	// the 16-bit twiddle half this wave's term multiplies by, as words (bit i of every bit-lane's
-	// half in word i): term 0 the low half, 1 the high half, 2 their sum
-	auto half_of = [&](uint32_t tw) -> uint32_t {
-		return term == 0 ? (tw & 0xFFFFu) : term == 1 ? (tw >> 16) : ((tw ^ (tw >> 16)) & 0xFFFFu);
+		__builtin_amdgcn_sched_barrier(0);
+		bsm4_mul(V, a, p);
+		bsm4_mul(V + 16, b, z);
+		__builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+		for (int i = 0; i < 16; i++) p[i] ^= z[i];
 	};
 	auto tile_tw = [&](int j, int q) -> uint32_t {
 		uint32_t tw = 0;
@@ -588,94 +575,85 @@ __global__ __launch_bounds__(kSplitNT, 1) void antt_bs3_pass(BsParams P) {
 		const int m = ps.stage_m[j];
 		const int qu = ((lane >> m) << (m + 1)) | (lane & ((1 << m) - 1));
 		const int qv = qu | (1 << m);
-		uint32_t* pu = plane + qu * kLimbStride;
-		uint32_t* pv = plane + qv * kLimbStride;
-		{
-			const uint32_t wt = half_of(cu_w[j] ^ tile_tw(j, qu));
-			uint32_t W[16];
+		const uint32_t* su = lds + cur * 4 * kPlane + l * kPlane + qu * kLimbStride;
+		const uint32_t* sv = lds + cur * 4 * kPlane + l * kPlane + qv * kLimbStride;
+		uint32_t* du = lds + (cur ^ 1) * 4 * kPlane + l * kPlane + qu * kLimbStride;
+		uint32_t* dv = lds + (cur ^ 1) * 4 * kPlane + l * kPlane + qv * kLimbStride;
+		uint32_t V[32], W0[16], W1[16], pr[16];
 #pragma unroll
-			for (int i = 0; i < 16; i++) W[i] = (uint32_t)__builtin_amdgcn_sbfe(wt, i, 1);
-			term_product(pv, pv + 16, W);
+		for (int i = 0; i < 32; i += 4) *(uint4*)(V + i) = *(const uint4*)(sv + i);
+		const uint32_t wt = cu_w[j] ^ tile_tw(j, qu);
+#pragma unroll
+		for (int i = 0; i < 16; i++) {
+			W0[i] = (uint32_t)__builtin_amdgcn_sbfe(wt, i, 1);
+			W1[i] = (uint32_t)__builtin_amdgcn_sbfe(wt, 16 + i, 1);
+		}
+		half_product(ps.field[j], V, W0, W1, pr);
+#pragma unroll
+		for (int i = 0; i < 16; i += 4) {
+			uint4 uu = *(const uint4*)(su + o + i);
+			uu.x ^= pr[i], uu.y ^= pr[i + 1], uu.z ^= pr[i + 2], uu.w ^= pr[i + 3];
+			*(uint4*)(du + o + i) = uu;
+			*(uint4*)(dv + o + i) = make_uint4(V[o + i] ^ uu.x, V[o + i + 1] ^ uu.y, V[o + i + 2] ^ uu.z, V[o + i + 3] ^ uu.w);
 		}
 		__syncthreads();
-		if (term < 2) {
-			uint32_t pr[16];
-			product_half(pr);
-			const int o = 16 * term;
-#pragma unroll
-			for (int i = 0; i < 16; i += 4) {
-				uint4 uu = *(const uint4*)(pu + o + i);
-				const uint4 vv = *(const uint4*)(pv + o + i);
-				uu.x ^= pr[i], uu.y ^= pr[i + 1], uu.z ^= pr[i + 2], uu.w ^= pr[i + 3];
-				*(uint4*)(pu + o + i) = uu;
-				*(uint4*)(pv + o + i) = make_uint4(vv.x ^ uu.x, vv.y ^ uu.y, vv.z ^ uu.z, vv.w ^ uu.w);
-			}
-		}
-		__syncthreads();
+		cur ^= 1;
 	}
 
 	if (LAST) {
 		// ---- stages 4..0 inside the words (antt_bs_pass's packing: lane owns blocks qa = lane and
 		// qb = lane + 64 of limb l; A's v-lanes move onto the u positions, B's stay)
 		const int qa = lane, qb = qa | (kTileBlocks / 2);
-		uint32_t* pa = plane + qa * kLimbStride;
-		uint32_t* pb = plane + qb * kLimbStride;
 		for (int s = 4; s >= ps.stop_j; s--) {
 			const uint32_t d = vgpr(1u << s);
 			const uint32_t um = vgpr(~lane_mask(s));
-			{
-				const uint32_t cb = cu_w[s] ^ tile_tw(s, qb);
-				uint32_t T[32], W[16];
+			const uint32_t* sa = lds + cur * 4 * kPlane + l * kPlane + qa * kLimbStride;
+			const uint32_t* sb = lds + cur * 4 * kPlane + l * kPlane + qb * kLimbStride;
+			uint32_t* da = lds + (cur ^ 1) * 4 * kPlane + l * kPlane + qa * kLimbStride;
+			uint32_t* db = lds + (cur ^ 1) * 4 * kPlane + l * kPlane + qb * kLimbStride;
+			const uint32_t cb = cu_w[s] ^ tile_tw(s, qb);
+			uint32_t T[32], W0[16], W1[16], pr[16];
 #pragma unroll
-				for (int i = 0; i < 32; i += 4) {
-					const uint4 a = *(const uint4*)(pa + i), b = *(const uint4*)(pb + i);
-					T[i] = __builtin_amdgcn_bitop3_b32(a.x >> d, b.x, um, 0xe4);
-					T[i + 1] = __builtin_amdgcn_bitop3_b32(a.y >> d, b.y, um, 0xe4);
-					T[i + 2] = __builtin_amdgcn_bitop3_b32(a.z >> d, b.z, um, 0xe4);
-					T[i + 3] = __builtin_amdgcn_bitop3_b32(a.w >> d, b.w, um, 0xe4);
-				}
-				// twiddle words: the bit-lane pattern plus the block part (antt_bs_pass), this term's half
+			for (int i = 0; i < 32; i += 4) {
+				const uint4 a = *(const uint4*)(sa + i), b = *(const uint4*)(sb + i);
+				T[i] = __builtin_amdgcn_bitop3_b32(a.x >> d, b.x, um, 0xe4);
+				T[i + 1] = __builtin_amdgcn_bitop3_b32(a.y >> d, b.y, um, 0xe4);
+				T[i + 2] = __builtin_amdgcn_bitop3_b32(a.z >> d, b.z, um, 0xe4);
+				T[i + 3] = __builtin_amdgcn_bitop3_b32(a.w >> d, b.w, um, 0xe4);
+			}
+			// twiddle words: the bit-lane pattern plus the block part (antt_bs_pass)
 #pragma unroll
-				for (int i = 0; i < 16; i++) {
-					const uint32_t lo = ps.pat[s][i] ^ (uint32_t)__builtin_amdgcn_sbfe(cb, i, 1);
-					const uint32_t hi = ps.pat[s][16 + i] ^ (uint32_t)__builtin_amdgcn_sbfe(cb, 16 + i, 1);
-					W[i] = term == 0 ? lo : term == 1 ? hi : lo ^ hi;
+			for (int i = 0; i < 16; i++) {
+				W0[i] = ps.pat[s][i] ^ (uint32_t)__builtin_amdgcn_sbfe(cb, i, 1);
+				W1[i] = ps.pat[s][16 + i] ^ (uint32_t)__builtin_amdgcn_sbfe(cb, 16 + i, 1);
+			}
+			half_product(ps.field[s], T, W0, W1, pr);
+#pragma unroll
+			for (int i = 0; i < 16; i += 4) {
+				uint32_t A[4], Bv[4];
+				*(uint4*)A = *(const uint4*)(sa + o + i);
+				*(uint4*)Bv = *(const uint4*)(sb + o + i);
+#pragma unroll
+				for (int c = 0; c < 4; c++) {
+					const uint32_t a = __builtin_amdgcn_bitop3_b32(pr[i + c], um, A[c], 0x6a);
+					const uint32_t b = __builtin_amdgcn_bitop3_b32(pr[i + c] >> d, um, Bv[c], 0x6a);
+					A[c] = __builtin_amdgcn_bitop3_b32(a << d, um, a, 0x9a);
+					Bv[c] = __builtin_amdgcn_bitop3_b32(b << d, um, b, 0x9a);
 				}
-				term_product(T, T + 16, W);
+				*(uint4*)(da + o + i) = *(const uint4*)A;
+				*(uint4*)(db + o + i) = *(const uint4*)Bv;
 			}
 			__syncthreads();
-			if (term < 2) {
-				uint32_t pr[16];
-				product_half(pr);
-				const int o = 16 * term;
-#pragma unroll
-				for (int i = 0; i < 16; i += 4) {
-					uint32_t A[4], Bv[4];
-					*(uint4*)A = *(const uint4*)(pa + o + i);
-					*(uint4*)Bv = *(const uint4*)(pb + o + i);
-#pragma unroll
-					for (int c = 0; c < 4; c++) {
-						const uint32_t a = __builtin_amdgcn_bitop3_b32(pr[i + c], um, A[c], 0x6a);
-						const uint32_t b = __builtin_amdgcn_bitop3_b32(pr[i + c] >> d, um, Bv[c], 0x6a);
-						A[c] = __builtin_amdgcn_bitop3_b32(a << d, um, a, 0x9a);
-						Bv[c] = __builtin_amdgcn_bitop3_b32(b << d, um, b, 0x9a);
-					}
-					*(uint4*)(pa + o + i) = *(const uint4*)A;
-					*(uint4*)(pb + o + i) = *(const uint4*)Bv;
-				}
-			}
-			__syncthreads();
+			cur ^= 1;
 		}
-		// back to compact words: 512 block transposes, one per thread
-		for (int g = tid; g < kTileBlocks * L; g += kSplitNT) {
-			uint32_t* x = lds + (g >> 7) * kPlane + (g & 127) * kLimbStride;
-			uint32_t r[32];
-#pragma unroll
-			for (int i = 0; i < 32; i += 4) *(uint4*)(r + i) = *(const uint4*)(x + i);
-			transpose32(r);
-#pragma unroll
-			for (int i = 0; i < 32; i += 4) *(uint4*)(x + i) = *(const uint4*)(r + i);
-		}
+	}
+	return cur;
+	};
+	const int cur = half == 0 ? stages(std::integral_constant<int, 0>()) : stages(std::integral_constant<int, 1>());
+	if (LAST) {
+		// back to compact words
+		uint32_t* const fin = lds + cur * 4 * kPlane;
+		transpose_blocks(fin);
 		__syncthreads();
 		for (int u = tid; u < kTileBlocks * 8 * L; u += kSplitNT) {
 			const int q = u / (8 * L), j = u % (8 * L);
@@ -683,14 +661,15 @@ __global__ __launch_bounds__(kSplitNT, 1) void antt_bs3_pass(BsParams P) {
 #pragma unroll
 			for (int c = 0; c < 4; c++) {
 				const int word = 4 * j + c;
-				wd[c] = lds[(word % L) * kPlane + q * kLimbStride + word / L];
+				wd[c] = fin[(word % L) * kPlane + q * kLimbStride + word / L];
 			}
 			if (!(BS_DBG(P) & 2)) st_stream(dst + (ooff | tile_off(q)) * L + 4 * j, make_uint4(wd[0], wd[1], wd[2], wd[3]));
 		}
 	} else {
+		const uint32_t* const fin = lds + cur * 4 * kPlane;
 		for (int u = tid; u < kTileBlocks * 8 * L; u += kSplitNT) {
 			const int pl = u >> 10, r = u & 1023, q = r >> 3, j = r & 7;
-			const uint4 g = *(const uint4*)(lds + pl * kPlane + q * kLimbStride + 4 * j);
+			const uint4 g = *(const uint4*)(fin + pl * kPlane + q * kLimbStride + 4 * j);
 			if (!(BS_DBG(P) & 2)) st_stream(dst + (ooff | tile_off(q)) * L + 32 * pl + 4 * j, g);
 		}
 	}
@@ -885,11 +864,14 @@ static BsDevKnobs dev_knobs() {
 	return k;
 }
 
-// GF(2^16/32) LDS-tile passes of fewer tiles than two per CU (one 2^20 transform) run lane-split
-// (antt_bs3_pass: three waves per product, three waves per SIMD instead of one)
+// GF(2^16/32) LDS-tile upper passes of fewer tiles than two per CU (one 2^20 transform) run
+// lane-split (antt_bs3_pass: two waves per product, two waves per SIMD instead of one). 2^20 A/B
+// (tools/ab_split.sh): upper GF(2^32) pass 0.0139 vs 0.0158 ms, bottom pass 0.0514 vs 0.0496 ms,
+// so the bottom pass keeps one wave per limb
 static bool use_split(const bn_antt_plan* plan, const BsPass& pass, size_t ntiles, const BsDevKnobs& kn) {
 	if (plan->limbs != 4 || pass_fmax(pass) <= 8) return false;
 	if (kn.split >= 0) return kn.split != 0;
+	if (pass.role == ROLE_LAST || pass.role == ROLE_SINGLE) return false;
 	return ntiles < (size_t)2 * (size_t)plan->num_cus;
 }
 

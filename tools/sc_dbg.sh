@@ -1,6 +1,7 @@
 #!/bin/bash
 # Timing experiments on the sumcheck kernels with the development library (make BN_DEV=1):
-# BN_SC_DBG=0..3 (bit 0: synthetic operands instead of column loads, bit 1: no products), one
+# BN_SC_DBG (bit 0: synthetic operands instead of column loads, bit 1: no products, bit 2: no
+# k-multiples, bit 3: no parity reduction), one
 # kernel-trace per setting; results are wrong by design. Output: gpurun_out/scdbg_<n>/
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -12,4 +13,5 @@ for n in ${SC_DBG_SET:-0 1 2 3}; do
   echo "== BN_SC_DBG=$n"; grep -h '"c4"' "$R/gpurun_out/scdbg_$n.log" | cut -c1-200
   f=$(find "$R/gpurun_out/scdbg_$n" -name '*kernel_stats.csv' | head -1)
   cut -d, -f1-4 "$f" | grep sc_ | sed 's/(bn::(anonymous namespace)::ScArgs)//'
+  python3 "$R/tools/sc_round_gaps.py" "$R/gpurun_out/scdbg_$n/run_kernel_trace.csv" 24 > "$R/gpurun_out/scdbg_rounds_$n.txt" && head -1 "$R/gpurun_out/scdbg_rounds_$n.txt" && tail -6 "$R/gpurun_out/scdbg_rounds_$n.txt"
 done
