@@ -53,6 +53,7 @@ constexpr int kAccSet = kAccCopies * kAccStride;
 // kResSeq (so the host polls one word instead of queueing a copy and synchronising the stream).
 constexpr int kAccCount = kAccStride - 1;
 constexpr size_t kPostInKernelMaxWG = 64;  // grids up to this post in-kernel (else sc_post)
+static_assert(kPostInKernelMaxWG <= (size_t)kAccCopies, "an in-kernel posting grid stores one copy per workgroup");
 constexpr size_t kHexMaxItems = 8192;      // launches up to this many items use 16-lane products
 using namespace quad;
 static_assert(kAccStride > 4 * (kMaxD + 1), "accumulator copy too small");
@@ -72,6 +73,20 @@ __device__ __forceinline__ void mul_small(const uint32_t* c, const uint32_t* x, 
 		}
 #pragma unroll
 		for (int b = 0; b < 4; b++) out[4 * g + b] = r[b];
+	}
+}
+
+// x <- k x for k = 2 or 3 (m = 0 or ~0: k = 2 + (m & 1)), the same map as mul_small with 8 XORs
+// per 4-word group instead of 16 AND-XORs: with X0^2 = X0 + 1, X0 (a0 + a1 X0) = a1 + (a0 + a1) X0 on
+// both GF(2^2) halves of each GF(2^4) coordinate, plus m & x
+__device__ __forceinline__ void mul_23(uint32_t m, uint32_t* x) {
+#pragma unroll
+	for (int g = 0; g < 8; g++) {
+		const uint32_t b0 = x[4 * g], b1 = x[4 * g + 1], b2 = x[4 * g + 2], b3 = x[4 * g + 3];
+		x[4 * g] = b1 ^ (b0 & m);
+		x[4 * g + 1] = b0 ^ (b1 & ~m);
+		x[4 * g + 2] = b3 ^ (b2 & m);
+		x[4 * g + 3] = b2 ^ (b3 & ~m);
 	}
 }
 
@@ -214,7 +229,12 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_messages(ScArgs A) {
 #ifdef BN_DEV
 				if (!(A.dbg & 4))
 #endif
-				mul_small(A.kcol[k], hi, hi);
+				{
+					if (A.kmax <= 3)  // d <= 3: every k here is 2 or 3 (launch-uniform branch)
+						mul_23(0u - (uint32_t)(k & 1), hi);
+					else
+						mul_small(A.kcol[k], hi, hi);
+				}
 #pragma unroll
 				for (int i = 0; i < 32; i++) lo[i] ^= hi[i];
 			}
@@ -254,24 +274,37 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_messages(ScArgs A) {
 		if (threadIdx.x == 0) __hip_atomic_store(A.res + kResSeq, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 		return;
 	}
-	// small grids: the last workgroup to finish reduces the copies and posts the points itself
-	if (threadIdx.x < 4 * (A.kmax + 1) && accL[threadIdx.x]) {
-		// a returning atomic: its value is back only once the XOR has been performed, which
-		// orders it before this workgroup's count below without a release fence
-		const uint32_t old = __hip_atomic_fetch_xor(A.acc + (blockIdx.x % kAccCopies) * kAccStride + threadIdx.x,
-													accL[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-		asm volatile("" ::"v"(old));
-	}
+	// small grids (<= kAccCopies workgroups): workgroup b stores its sums into copy b with plain
+	// stores, the last one to finish XORs the gridDim.x copies and posts the points itself
+	const int nw = 4 * (A.kmax + 1);
+	if (threadIdx.x < nw) A.acc[blockIdx.x * kAccStride + threadIdx.x] = accL[threadIdx.x];
 	uint32_t* last = accL + 4 * (kMaxD + 1);  // (a static __shared__ word cost a workgroup per CU)
 	__syncthreads();
 	if (threadIdx.x == 0)
-		// acq_rel: release orders this workgroup's XORs before its count, acquire makes every other
-		// workgroup's XORs visible to the last one (once per round, so the cost does not matter)
+		// acq_rel: release orders this workgroup's stores before its count, acquire makes every other
+		// workgroup's stores visible to the last one
 		*last = __hip_atomic_fetch_add(A.acc + kAccCount, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
 	__syncthreads();
 	if (!*last) return;
 	__threadfence();
-	post_points(A, threadIdx.x);
+	uint32_t* red = last + 1;  // 4 (kMaxD + 1) words
+	if (threadIdx.x < nw) red[threadIdx.x] = 0;
+	__syncthreads();
+	// every (copy, word) by one thread, XOR-reduced in LDS
+	for (int i = threadIdx.x; i < (int)gridDim.x * nw; i += kScThreads) {
+		const int b = i / nw, w = i - b * nw;
+		const uint32_t v = __hip_atomic_load(A.acc + b * kAccStride + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if (v) atomicXor(red + w, v);
+	}
+	__syncthreads();
+	if (threadIdx.x < nw) {
+		A.res[threadIdx.x] = red[threadIdx.x];
+		if (A.sink) A.sink[threadIdx.x] = red[threadIdx.x];
+	}
+	if (A.sink && threadIdx.x == 0) A.sink[kResSeq] = (uint32_t)A.skip1 | (A.mode == 2 ? 2u : 0u);
+	__threadfence_system();
+	__syncthreads();
+	if (threadIdx.x == 0) __hip_atomic_store(A.res + kResSeq, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Big grids: a one-wave kernel after sc_messages reduces the copies and posts the points (one
@@ -355,9 +388,10 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_coal(ScArgs A) {
 	}
 }
 
-// quad slots + the fold's broadcast challenge (128 words) + the messages' accumulators and flag
+// quad slots + the fold's broadcast challenge (128 words) + the messages' accumulators, flag and
+// last-workgroup reduction
 template <int G>
-size_t lds_bytes() { return ((size_t)Grp<G>::kSlotsWords + 128 + 4 * (kMaxD + 1) + 1) * sizeof(uint32_t); }
+size_t lds_bytes() { return ((size_t)Grp<G>::kSlotsWords + 128 + 8 * (kMaxD + 1) + 1) * sizeof(uint32_t); }
 
 struct DeviceScope {
 	int prev = -1;
@@ -449,8 +483,17 @@ int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 		A.dbg = dbg;
 	}
 #endif
-	for (int k = 0; k <= kMaxD; k++)
-		for (int a = 0; a < 4; a++) A.kcol[k][a] = (uint32_t)tw_mul((uint64_t)k, 1ull << a, 2);
+	// GF(2^4) products k * 2^a, tabulated once (36 recursive tower products per launch were ~1 us of
+	// host time on every round's critical path)
+	struct KCol {
+		uint32_t v[kMaxD + 1][4];
+		KCol() {
+			for (int k = 0; k <= kMaxD; k++)
+				for (int a = 0; a < 4; a++) v[k][a] = (uint32_t)tw_mul((uint64_t)k, 1ull << a, 2);
+		}
+	};
+	static const KCol kc;
+	memcpy(A.kcol, kc.v, sizeof A.kcol);
 	// one item per lane group: fold (column, pair), messages (pair, point)
 	const size_t items = fold ? (size_t)sc->d * A.n_pairs : A.n_pairs * (size_t)(A.kmax + 1 - A.skip1);
 	size_t hex_max = kHexMaxItems, post_max = kPostInKernelMaxWG;
@@ -458,7 +501,7 @@ int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 	{
 		static const char *eh = getenv("BN_SC_HEX_MAX"), *ep = getenv("BN_SC_POST_MAX");
 		if (eh) hex_max = (size_t)atol(eh);
-		if (ep) post_max = (size_t)atol(ep);
+		if (ep) post_max = std::min((size_t)atol(ep), (size_t)kAccCopies);
 	}
 #endif
 	const bool hex = items <= hex_max;
