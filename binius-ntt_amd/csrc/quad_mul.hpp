@@ -213,5 +213,110 @@ __device__ __forceinline__ void hex_mul(const Slot& S, const uint32_t* B, int s)
 	wsync();
 }
 
+// Lowest-latency GF(2^128) product on a whole wave, for the sumcheck's smallest launches (a few
+// hundred items: one wave per SIMD or less, so latency is all that counts). The GF(2^32)
+// products of hex_mul are themselves split by Karatsuba over GF(2^16): 36 bsm4 circuits
+// (316 gates) side by side instead of 12 bsm5 circuits (1022), then one more combine phase.
+//   lane s < 36: q = s / 9, t = s / 3 % 3 (hex_mul's (q, t)), u = s % 3 (GF(2^16) term: lo, hi, sum)
+//   lane s < 12: GF(2^32) product (q, t) = s: lo = z0 + z2, hi = z1 + z0 + z2 + alpha(z2) over its
+//                three GF(2^16) products, into hex_mul's z rows (and alpha(z2) for t = 1)
+//   then hex_mul's last two phases (P halves, limbs).
+// Slot: hex_mul's 24 rows, then 36 GF(2^16) products of 16 words at a 20-word stride.
+constexpr int kWideZ16 = 24 * kRowWords;
+constexpr int kWideWords = kWideZ16 + 36 * 20 + 16;
+
+template <bool B_SHARED>
+__device__ __forceinline__ void wide_mul(const Slot& S, const uint32_t* B, int s) {
+	wsync();
+	if (s < 36) {
+		const int q = s / 9, t = (s / 3) % 3, u = s % 3;
+		const int ia = q & 1, jb = (q == 1 || q == 2) ? 1 : 0;
+		const int ra = 2 * ia + (t == 1), rb = 2 * jb + (t == 1);
+		const uint32_t m = t == 2 ? ~0u : 0u;
+		const uint32_t* A0 = S.row(ra);
+		const uint32_t* A1 = S.row(2 * ia + 1);
+		const uint32_t* B0 = B_SHARED ? B + 32 * rb : S.row(4 + rb);
+		const uint32_t* B1 = B_SHARED ? B + 64 * jb + 32 : S.row(4 + 2 * jb + 1);
+		// the GF(2^32) operands of (q, t) as in hex_mul, then their GF(2^16) half or half-sum u
+		const uint32_t mlo = u == 1 ? 0u : ~0u, mhi = u == 0 ? 0u : ~0u;
+		uint32_t x[16], y[16], z[16];
+#pragma unroll
+		for (int i = 0; i < 16; i += 4) {
+			const uint4 p = *(const uint4*)(A0 + i), p1 = *(const uint4*)(A1 + i);
+			const uint4 ph = *(const uint4*)(A0 + 16 + i), p1h = *(const uint4*)(A1 + 16 + i);
+			const uint4 v = *(const uint4*)(B0 + i), v1 = *(const uint4*)(B1 + i);
+			const uint4 vh = *(const uint4*)(B0 + 16 + i), v1h = *(const uint4*)(B1 + 16 + i);
+			x[i] = ((p.x ^ (p1.x & m)) & mlo) ^ ((ph.x ^ (p1h.x & m)) & mhi);
+			x[i + 1] = ((p.y ^ (p1.y & m)) & mlo) ^ ((ph.y ^ (p1h.y & m)) & mhi);
+			x[i + 2] = ((p.z ^ (p1.z & m)) & mlo) ^ ((ph.z ^ (p1h.z & m)) & mhi);
+			x[i + 3] = ((p.w ^ (p1.w & m)) & mlo) ^ ((ph.w ^ (p1h.w & m)) & mhi);
+			y[i] = ((v.x ^ (v1.x & m)) & mlo) ^ ((vh.x ^ (v1h.x & m)) & mhi);
+			y[i + 1] = ((v.y ^ (v1.y & m)) & mlo) ^ ((vh.y ^ (v1h.y & m)) & mhi);
+			y[i + 2] = ((v.z ^ (v1.z & m)) & mlo) ^ ((vh.z ^ (v1h.z & m)) & mhi);
+			y[i + 3] = ((v.w ^ (v1.w & m)) & mlo) ^ ((vh.w ^ (v1h.w & m)) & mhi);
+		}
+		__builtin_amdgcn_sched_barrier(0);
+		bsm4_mul(x, y, z);
+		__builtin_amdgcn_sched_barrier(0);
+		uint32_t* zo = S.base + kWideZ16 + 20 * s;
+#pragma unroll
+		for (int i = 0; i < 16; i += 4) *(uint4*)(zo + i) = make_uint4(z[i], z[i + 1], z[i + 2], z[i + 3]);
+	}
+	wsync();
+	if (s < 12) {
+		const int q = s / 3, t = s - 3 * (s / 3);
+		const uint32_t* zb = S.base + kWideZ16 + 20 * (3 * s);
+		uint32_t z0[16], z2[16], z1[16], al[16], r[32];
+#pragma unroll
+		for (int i = 0; i < 16; i += 4) {
+			*(uint4*)(z0 + i) = *(const uint4*)(zb + i);
+			*(uint4*)(z2 + i) = *(const uint4*)(zb + 20 + i);
+			*(uint4*)(z1 + i) = *(const uint4*)(zb + 40 + i);
+		}
+		bs_alpha<4>(z2, al);
+#pragma unroll
+		for (int i = 0; i < 16; i++) {
+			r[i] = z0[i] ^ z2[i];
+			r[16 + i] = z1[i] ^ r[i] ^ al[i];
+		}
+		sst(S, 8 + s, r);
+		if (t == 1) {
+			uint32_t a[32];
+			bs_alpha<5>(r, a);
+			sst(S, 20 + q, a);
+		}
+	}
+	wsync();
+	if (s < 8) {  // P_q.lo = z0 + z2, P_q.hi = P_q.lo + z1 + alpha(z2)   (as hex_mul)
+		const int q = s >> 1;
+		const uint32_t m = (s & 1) ? ~0u : 0u;
+		const uint32_t *z0 = S.row(8 + 3 * q), *z2 = S.row(9 + 3 * q), *z1 = S.row(10 + 3 * q), *az = S.row(20 + q);
+		uint32_t r[32];
+#pragma unroll
+		for (int i = 0; i < 32; i++) r[i] = z0[i] ^ z2[i] ^ ((z1[i] ^ az[i]) & m);
+		wsync();
+		sst(S, 4 + s, r);
+	}
+	wsync();
+	if (s < 4) {
+		const int h = s & 1, qa = s < 2 ? 0 : 2;
+		const uint32_t m2 = s >= 2 ? ~0u : 0u;
+		const uint32_t *pa = S.row(4 + 2 * qa + h), *pb = S.row(6 + 2 * qa + h), *pc = S.row(s == 2 ? 7 : 6);
+		uint32_t r[32];
+#pragma unroll
+		for (int i = 0; i < 32; i++) r[i] = pa[i] ^ pb[i] ^ (pc[i] & m2);
+		if (s == 3) {
+			uint32_t x[32], y[32];
+			sld(x, S, 7);
+			bs_alpha<5>(x, y);
+#pragma unroll
+			for (int i = 0; i < 32; i++) r[i] ^= y[i];
+		}
+		wsync();
+		sst(S, s, r);
+	}
+	wsync();
+}
+
 }  // namespace quad
 }  // namespace bn

@@ -55,6 +55,7 @@ constexpr int kAccCount = kAccStride - 1;
 constexpr size_t kPostInKernelMaxWG = 64;  // grids up to this post in-kernel (else sc_post)
 static_assert(kPostInKernelMaxWG <= (size_t)kAccCopies, "an in-kernel posting grid stores one copy per workgroup");
 constexpr size_t kHexMaxItems = 8192;      // launches up to this many items use 16-lane products
+constexpr size_t kWideMaxItems = 1024;     // ... and up to this many the 64-lane product
 using namespace quad;
 static_assert(kAccStride > 4 * (kMaxD + 1), "accumulator copy too small");
 constexpr int kResSeq = 4 * (kMaxD + 1);
@@ -177,20 +178,23 @@ __device__ __forceinline__ void post_points(const ScArgs& A, int t) {
 }
 
 // Products run on a group of G lanes: G = 4 (quad_mul, throughput) for launches that fill the
-// GPU, G = 16 (hex_mul, about a third of the latency) for the last rounds' small launches. Lanes
-// l < 4 of a group hold the limbs of the operands and results.
+// GPU, G = 16 (hex_mul, about a third of the latency) for the last rounds' small launches, G = 64
+// (wide_mul, GF(2^16) circuits on 36 lanes) for the smallest. Lanes l < 4 of a group hold the
+// limbs of the operands and results.
 template <int G>
 struct Grp {
 	static constexpr int kGroups = kScThreads / G;
-	static constexpr int kSlotWords = G == 4 ? kQuadWords : kHexWords;
+	static constexpr int kSlotWords = G == 4 ? kQuadWords : G == 16 ? kHexWords : kWideWords;
 	static constexpr int kSlotsWords = kGroups * kSlotWords;
 };
 template <int G, bool B_SHARED>
 __device__ __forceinline__ void grp_mul(const Slot& S, const uint32_t* B, int l) {
 	if constexpr (G == 4)
 		quad_mul<B_SHARED>(S, B, l);
-	else
+	else if constexpr (G == 16)
 		hex_mul<B_SHARED>(S, B, l);
+	else
+		wide_mul<B_SHARED>(S, B, l);
 }
 
 // One (pair, point k) per group, k fastest: the kmax+1 groups of a pair run side by side, so the
@@ -496,27 +500,32 @@ int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 	memcpy(A.kcol, kc.v, sizeof A.kcol);
 	// one item per lane group: fold (column, pair), messages (pair, point)
 	const size_t items = fold ? (size_t)sc->d * A.n_pairs : A.n_pairs * (size_t)(A.kmax + 1 - A.skip1);
-	size_t hex_max = kHexMaxItems, post_max = kPostInKernelMaxWG;
+	size_t hex_max = kHexMaxItems, wide_max = kWideMaxItems, post_max = kPostInKernelMaxWG;
 #ifdef BN_DEV
 	{
-		static const char *eh = getenv("BN_SC_HEX_MAX"), *ep = getenv("BN_SC_POST_MAX");
+		static const char *eh = getenv("BN_SC_HEX_MAX"), *ew = getenv("BN_SC_WIDE_MAX"), *ep = getenv("BN_SC_POST_MAX");
 		if (eh) hex_max = (size_t)atol(eh);
+		if (ew) wide_max = (size_t)atol(ew);
 		if (ep) post_max = std::min((size_t)atol(ep), (size_t)kAccCopies);
 	}
 #endif
-	const bool hex = items <= hex_max;
-	const size_t per_wg = hex ? Grp<16>::kGroups : Grp<4>::kGroups;
+	// 64-, 16-, 4-lane products; folds stay on 16 lanes (one product each: the 64-lane product's
+	// extra combine phase cost what its shorter circuit saved, c4 trace of round 4)
+	const int tier = (!fold && items <= wide_max) ? 2 : items <= hex_max ? 1 : 0;
+	const size_t per_wg = tier == 2 ? Grp<64>::kGroups : tier == 1 ? Grp<16>::kGroups : Grp<4>::kGroups;
 	const size_t grid = (items + per_wg - 1) / per_wg;
 	void* args[] = {&A};
-	const bool coal = fold && !hex && A.mode == 0 && A.n_pairs % 16 == 0;
-	const void* fns[2][2][3] = {
+	const bool coal = fold && tier == 0 && A.mode == 0 && A.n_pairs % 16 == 0;
+	const void* fns[3][2][3] = {
 		{{(const void*)sc_messages<0, 4>, (const void*)sc_messages<1, 4>, (const void*)sc_messages<2, 4>},
 		 {coal ? (const void*)sc_fold_coal : (const void*)sc_fold<0, 4>, (const void*)sc_fold<1, 4>, (const void*)sc_fold<2, 4>}},
 		{{(const void*)sc_messages<0, 16>, (const void*)sc_messages<1, 16>, (const void*)sc_messages<2, 16>},
-		 {(const void*)sc_fold<0, 16>, (const void*)sc_fold<1, 16>, (const void*)sc_fold<2, 16>}}};
+		 {(const void*)sc_fold<0, 16>, (const void*)sc_fold<1, 16>, (const void*)sc_fold<2, 16>}},
+		{{(const void*)sc_messages<0, 64>, (const void*)sc_messages<1, 64>, (const void*)sc_messages<2, 64>},
+		 {(const void*)sc_fold<0, 16>, (const void*)sc_fold<1, 16>, (const void*)sc_fold<2, 16>}}};  // (not used)
 	A.post = grid <= post_max;
-	BN_HIP(hipLaunchKernel(fns[hex][fold ? 1 : 0][A.mode], dim3((unsigned)grid), dim3(kScThreads), args,
-						   hex ? lds_bytes<16>() : lds_bytes<4>(), sc->stream));
+	const size_t lds = tier == 2 ? lds_bytes<64>() : tier == 1 ? lds_bytes<16>() : lds_bytes<4>();
+	BN_HIP(hipLaunchKernel(fns[tier][fold ? 1 : 0][A.mode], dim3((unsigned)grid), dim3(kScThreads), args, lds, sc->stream));
 	if (!fold && !A.post) BN_HIP(hipLaunchKernel((const void*)sc_post, dim3(1), dim3(64), args, 0, sc->stream));
 	return BN_OK;
 }
@@ -542,13 +551,14 @@ int sc_common_init(bn_sumcheck* sc) {
 	BN_HIP(hipHostMalloc((void**)&sc->h_res, sizeof(uint32_t) * (kResSeq + 1), hipHostMallocMapped | hipHostMallocCoherent));
 	memset(sc->h_res, 0, sizeof(uint32_t) * (kResSeq + 1));
 	BN_HIP(hipHostGetDevicePointer((void**)&sc->d_res, sc->h_res, 0));
-	const void* fns[13] = {(const void*)sc_messages<0, 4>,  (const void*)sc_messages<1, 4>,  (const void*)sc_messages<2, 4>,
+	const void* fns[16] = {(const void*)sc_messages<0, 4>,  (const void*)sc_messages<1, 4>,  (const void*)sc_messages<2, 4>,
 						   (const void*)sc_fold<0, 4>,      (const void*)sc_fold<1, 4>,      (const void*)sc_fold<2, 4>,
 						   (const void*)sc_messages<0, 16>, (const void*)sc_messages<1, 16>, (const void*)sc_messages<2, 16>,
 						   (const void*)sc_fold<0, 16>,     (const void*)sc_fold<1, 16>,     (const void*)sc_fold<2, 16>,
+						   (const void*)sc_messages<0, 64>, (const void*)sc_messages<1, 64>, (const void*)sc_messages<2, 64>,
 						   (const void*)sc_fold_coal};
-	for (const void* f : fns)
-		BN_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max(lds_bytes<4>(), lds_bytes<16>())));
+	const int lds_max = (int)std::max(lds_bytes<4>(), std::max(lds_bytes<16>(), lds_bytes<64>()));
+	for (const void* f : fns) BN_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
 	return BN_OK;
 }
 
