@@ -452,6 +452,17 @@ __global__ __launch_bounds__(kSplitNT, 1) void antt_bs3_pass(BsParams P) {
 	const BsPass& ps = P.p;
 	const int tid = threadIdx.x;
 	const int w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+	// BN_TRACE (development build): per-wave cycles of load, block stages, in-word stages +
+	// transposes, store
+	const bool TR = BS_TRACE(P);
+	unsigned long long tr[4] = {0, 0, 0, 0}, tlast = TR ? __builtin_amdgcn_s_memtime() : 0;
+	auto mark = [&](int k) {
+		if (!TR) return;
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+		const unsigned long long t = __builtin_amdgcn_s_memtime();
+		tr[k] += t - tlast;
+		tlast = t;
+	};
 	const int l = w & 3, half = w >> 2;  // limb plane, product half
 	uint32_t* const cu_w = lds + 8 * kPlane;  // workgroup-uniform twiddle part per stage
 	const size_t n = (size_t)1 << P.log_h;
@@ -599,6 +610,7 @@ __global__ __launch_bounds__(kSplitNT, 1) void antt_bs3_pass(BsParams P) {
 		__syncthreads();
 		cur ^= 1;
 	}
+	mark(1);
 
 	if (LAST) {
 		// ---- stages 4..0 inside the words (antt_bs_pass's packing: lane owns blocks qa = lane and
@@ -649,7 +661,9 @@ __global__ __launch_bounds__(kSplitNT, 1) void antt_bs3_pass(BsParams P) {
 	}
 	return cur;
 	};
+	mark(0);
 	const int cur = half == 0 ? stages(std::integral_constant<int, 0>()) : stages(std::integral_constant<int, 1>());
+	mark(2);
 	if (LAST) {
 		// back to compact words
 		uint32_t* const fin = lds + cur * 4 * kPlane;
@@ -672,6 +686,11 @@ __global__ __launch_bounds__(kSplitNT, 1) void antt_bs3_pass(BsParams P) {
 			const uint4 g = *(const uint4*)(fin + pl * kPlane + q * kLimbStride + 4 * j);
 			if (!(BS_DBG(P) & 2)) st_stream(dst + (ooff | tile_off(q)) * L + 32 * pl + 4 * j, g);
 		}
+	}
+	mark(3);
+	if (TR && lane == 0) {
+		unsigned long long* o = P.trace + ((size_t)blockIdx.x * (kSplitNT / 64) + w) * 8;
+		o[0] = tr[0], o[1] = tr[1], o[2] = tr[2], o[3] = tr[3], o[4] = 1, o[5] = 0, o[6] = 0, o[7] = 0;
 	}
 }
 
@@ -893,11 +912,28 @@ static int launch_one(bn_antt_plan* plan, const BsPass& pass, int i, const uint3
 	if (use_split(plan, pass, ntiles, kn)) {
 		prm.ntiles = ntiles;
 		prm.trace = nullptr;
+		static unsigned long long* strbuf = nullptr;
+		if (kn.trace) {
+			if (!strbuf) BN_HIP(hipMalloc(&strbuf, (size_t)1 << 26));
+			BN_HIP(hipMemset(strbuf, 0, ntiles * 8 * 8 * 8));
+			prm.trace = strbuf;
+		}
 		int rc = timing_begin(plan, i, st);
 		if (rc != BN_OK) return rc;
 		void* args[] = {&prm};
 		BN_HIP(hipLaunchKernel(split_kernel_for(pass.role), dim3((unsigned)ntiles), dim3(kSplitNT), args, split_lds_bytes(), st));
-		return timing_end(plan, i, st);
+		rc = timing_end(plan, i, st);
+		if (rc != BN_OK || !prm.trace) return rc;
+		std::vector<unsigned long long> h(ntiles * 8 * 8);
+		BN_HIP(hipStreamSynchronize(st));
+		BN_HIP(hipMemcpy(h.data(), prm.trace, h.size() * 8, hipMemcpyDeviceToHost));
+		double acc[5] = {0};
+		for (size_t wv = 0; wv < ntiles * 8; wv++)
+			for (int k = 0; k < 5; k++) acc[k] += (double)h[wv * 8 + k];
+		const double t = acc[4] > 0 ? acc[4] : 1;
+		fprintf(stderr, "trace pass %d (split, %zu waves, cycles per wave): load %.0f  block %.0f  inword+tr %.0f  store %.0f\n", i,
+		        (size_t)acc[4], acc[0] / t, acc[1] / t, acc[2] / t, acc[3] / t);
+		return BN_OK;
 	}
 	// two 74-KB tiles per CU: a persistent grid of two workgroups per CU walks all tiles
 	const int fmax = pass_fmax(pass);
