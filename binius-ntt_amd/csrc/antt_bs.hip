@@ -441,6 +441,7 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 // antt_bs_pass.
 // ------------------------------------------------------------------------------------
 constexpr int kSplitNT = 512;  // 8 waves
+#define BS3_SB() __builtin_amdgcn_sched_barrier(0)
 static size_t split_lds_bytes() { return ((size_t)8 * kPlane + (size_t)kMaxStages) * sizeof(uint32_t); }
 
 template <int ROLE>
@@ -455,7 +456,7 @@ __global__ __launch_bounds__(kSplitNT, 1) void antt_bs3_pass(BsParams P) {
 	// BN_TRACE (development build): per-wave cycles of load, block stages, in-word stages +
 	// transposes, store
 	const bool TR = BS_TRACE(P);
-	unsigned long long tr[4] = {0, 0, 0, 0}, tlast = TR ? __builtin_amdgcn_s_memtime() : 0;
+	unsigned long long tr[6] = {0, 0, 0, 0, 0, 0}, tlast = TR ? __builtin_amdgcn_s_memtime() : 0;
 	auto mark = [&](int k) {
 		if (!TR) return;
 		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -544,16 +545,16 @@ __global__ __launch_bounds__(kSplitNT, 1) void antt_bs3_pass(BsParams P) {
 	// (the stage's `field`, wave-uniform) leave W1 zero: half h is then V's half h times W0 alone
 	auto half_product = [&](int field, const uint32_t* V, const uint32_t* W0, const uint32_t* W1, uint32_t* p) {
 		if (field <= 8) {
-			__builtin_amdgcn_sched_barrier(0);
+			BS3_SB();
 			bsm3_mul(V + o, W0, p);
 			bsm3_mul(V + o + 8, W0, p + 8);
-			__builtin_amdgcn_sched_barrier(0);
+			BS3_SB();
 			return;
 		}
 		if (field <= 16) {
-			__builtin_amdgcn_sched_barrier(0);
+			BS3_SB();
 			bsm4_mul(V + o, W0, p);
-			__builtin_amdgcn_sched_barrier(0);
+			BS3_SB();
 			return;
 		}
 		uint32_t a[16], b[16], z[16];
@@ -566,10 +567,10 @@ __global__ __launch_bounds__(kSplitNT, 1) void antt_bs3_pass(BsParams P) {
 #pragma unroll
 			for (int i = 0; i < 16; i++) a[i] = W1[i], b[i] = W0[i] ^ al[i];
 		}
-		__builtin_amdgcn_sched_barrier(0);
+		BS3_SB();
 		bsm4_mul(V, a, p);
 		bsm4_mul(V + 16, b, z);
-		__builtin_amdgcn_sched_barrier(0);
+		BS3_SB();
 #pragma unroll
 		for (int i = 0; i < 16; i++) p[i] ^= z[i];
 	};
@@ -599,7 +600,9 @@ __global__ __launch_bounds__(kSplitNT, 1) void antt_bs3_pass(BsParams P) {
 			W0[i] = (uint32_t)__builtin_amdgcn_sbfe(wt, i, 1);
 			W1[i] = (uint32_t)__builtin_amdgcn_sbfe(wt, 16 + i, 1);
 		}
+		if (TR) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); tr[4] -= __builtin_amdgcn_s_memtime(); }
 		half_product(ps.field[j], V, W0, W1, pr);
+		if (TR) { uint32_t acc = 0; for (int q = 0; q < 16; q++) acc ^= pr[q]; asm volatile("" ::"v"(acc)); tr[4] += __builtin_amdgcn_s_memtime(); }
 #pragma unroll
 		for (int i = 0; i < 16; i += 4) {
 			uint4 uu = *(const uint4*)(su + o + i);
@@ -690,7 +693,7 @@ __global__ __launch_bounds__(kSplitNT, 1) void antt_bs3_pass(BsParams P) {
 	mark(3);
 	if (TR && lane == 0) {
 		unsigned long long* o = P.trace + ((size_t)blockIdx.x * (kSplitNT / 64) + w) * 8;
-		o[0] = tr[0], o[1] = tr[1], o[2] = tr[2], o[3] = tr[3], o[4] = 1, o[5] = 0, o[6] = 0, o[7] = 0;
+		o[0] = tr[0], o[1] = tr[1], o[2] = tr[2], o[3] = tr[3], o[4] = 1, o[5] = tr[4], o[6] = 0, o[7] = 0;
 	}
 }
 
@@ -927,12 +930,12 @@ static int launch_one(bn_antt_plan* plan, const BsPass& pass, int i, const uint3
 		std::vector<unsigned long long> h(ntiles * 8 * 8);
 		BN_HIP(hipStreamSynchronize(st));
 		BN_HIP(hipMemcpy(h.data(), prm.trace, h.size() * 8, hipMemcpyDeviceToHost));
-		double acc[5] = {0};
+		double acc[6] = {0};
 		for (size_t wv = 0; wv < ntiles * 8; wv++)
-			for (int k = 0; k < 5; k++) acc[k] += (double)h[wv * 8 + k];
+			for (int k = 0; k < 6; k++) acc[k] += (double)h[wv * 8 + k];
 		const double t = acc[4] > 0 ? acc[4] : 1;
-		fprintf(stderr, "trace pass %d (split, %zu waves, cycles per wave): load %.0f  block %.0f  inword+tr %.0f  store %.0f\n", i,
-		        (size_t)acc[4], acc[0] / t, acc[1] / t, acc[2] / t, acc[3] / t);
+		fprintf(stderr, "trace pass %d (split, %zu waves, cycles per wave): load %.0f  block %.0f [mul %.0f]  inword+tr %.0f  store %.0f\n", i,
+		        (size_t)acc[4], acc[0] / t, acc[1] / t, acc[5] / t, acc[2] / t, acc[3] / t);
 		return BN_OK;
 	}
 	// two 74-KB tiles per CU: a persistent grid of two workgroups per CU walks all tiles
