@@ -14,7 +14,7 @@ circuit (1022 gates per 32 products, 243 of them ANDs with twiddle-bit masks). I
   * the pre-sums and the recombination of the 9 products are emitted with the same XOR3 fusion as
     the multiplier circuits (gen_bitsliced.py's Emitter), the accumulation into u included.
 
-Output: binius-ntt_amd/csrc/uniform_gen.hpp (bn::gf8c_mul, bn::bsm5_fma_uniform).
+Output: binius-ntt_amd/tools/uniform_gen.hpp (bn::gf8c_mul, bn::bsm5_fma_uniform; microbench6 only, not committed).
 """
 import os
 import sys
@@ -22,7 +22,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import gen_bitsliced as G  # noqa: E402
 
-OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "uniform_gen.hpp")
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "uniform_gen.hpp")
 
 
 def mul_alpha_int(a, h):

@@ -7,7 +7,7 @@
 // Both run the same dependent butterfly chain (u ^= t v; v ^= u) with the same uniform twiddle
 // sequence, so their final states must be bit-identical (checked). Prints lane-products/s and
 // cycles per wave-product at 2, 3 and 4 waves per SIMD.
-// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I../csrc microbench6.hip -o microbench6
+// Build: python3 gen_uniform.py && hipcc -O3 -std=c++17 --offload-arch=gfx950 -I../csrc microbench6.hip -o microbench6
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
