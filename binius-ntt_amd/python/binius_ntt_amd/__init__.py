@@ -508,7 +508,7 @@ class Sumcheck:
         """staged=True (host evals only): copy the columns but leave compact input untransposed until
         prepare() (or the first round) — the reference constructor's separate Memcpy and Transpose
         phases (sumcheck.cuh:88-124)."""
-        self.num_vars, self.d = num_vars, composition_size
+        self.num_vars, self.d, self.device = num_vars, composition_size, device
         p = ctypes.c_void_p()
         if isinstance(evals, np.ndarray):
             ev = np.ascontiguousarray(evals, dtype=np.uint32).reshape(-1)
@@ -558,7 +558,7 @@ class Sumcheck:
         elif device is None:
             device = 0
         self = cls.__new__(cls)
-        self.num_vars, self.d = num_vars, composition_size
+        self.num_vars, self.d, self.device = num_vars, composition_size, device
         p = ctypes.c_void_p()
         _check(lib().bn_sumcheck_create_shard_device(device, num_vars, composition_size, rank, world,
                                                      _ptr(local_evals), _stream(stream, local_evals.device.index),

@@ -107,6 +107,9 @@ class ShardedSumcheck:
         numpy -> pinned -> H2D hop per round;
       * host (gloo, or a prover without a sink): the words the prover returned are staged through
         WordExchange.
+    device_exchange=True on a gloo group keeps the device path's protocol (sink, flags, p(1) from
+    the global claim) and stages only the sink through host memory for the CPU collective: the
+    world-2 gloo GPU test runs the multi-rank device path that way.
     exchange_at_world1=True runs the exchange even when the group has one rank (the RCCL rehearsal
     on a one-GPU box exercises the device path that way)."""
 
@@ -126,10 +129,16 @@ class ShardedSumcheck:
         self._last_pts = None  # previous round's global points (device path)
         if self.device_exchange:
             import torch
-            dev = _device_for(dist, group)
-            self._sink = torch.zeros(SINK_WORDS, dtype=torch.int32, device=dev)
-            self._recv = torch.empty(self.world * SINK_WORDS, dtype=torch.int32, device=dev)
-            self._h_recv = torch.empty(self.world * SINK_WORDS, dtype=torch.int32, pin_memory=True)
+            pdev = torch.device("cuda", prover.device if getattr(prover, "device", None) is not None
+                                else torch.cuda.current_device())
+            self._stage = _device_for(dist, group).type != "cuda"  # a CPU collective (gloo)
+            self._sink = torch.zeros(SINK_WORDS, dtype=torch.int32, device=pdev)
+            if self._stage:
+                self._send = torch.empty(SINK_WORDS, dtype=torch.int32)
+                self._recv = torch.empty(self.world * SINK_WORDS, dtype=torch.int32)
+            else:
+                self._recv = torch.empty(self.world * SINK_WORDS, dtype=torch.int32, device=pdev)
+                self._h_recv = torch.empty(self.world * SINK_WORDS, dtype=torch.int32, pin_memory=True)
             prover.set_message_sink(self._sink)
 
     def _gather_if_needed(self):
@@ -152,9 +161,14 @@ class ShardedSumcheck:
         # sequence number, which the posting workgroup releases at system scope after writing the
         # sink words, and the collective's kernel is dispatched after that (with the dispatch's
         # acquire), so it reads the complete words
-        dist.all_gather_into_tensor(self._recv, self._sink, group=self.group)
-        self._h_recv.copy_(self._recv)  # synchronous: the host needs the words now
-        g = self._h_recv.numpy().view(np.uint32).reshape(self.world, SINK_WORDS)
+        if self._stage:
+            self._send.copy_(self._sink)  # synchronous device -> host
+            dist.all_gather_into_tensor(self._recv, self._send, group=self.group)
+            g = self._recv.numpy().view(np.uint32).reshape(self.world, SINK_WORDS)
+        else:
+            dist.all_gather_into_tensor(self._recv, self._sink, group=self.group)
+            self._h_recv.copy_(self._recv)  # synchronous: the host needs the words now
+            g = self._h_recv.numpy().view(np.uint32).reshape(self.world, SINK_WORDS)
         raw = np.bitwise_xor.reduce(g[:, :4 * d1], axis=0).reshape(d1, 4).copy()
         flags = int(g[0, 36])
         if flags & 2:  # the last call (one evaluation left): words 0-3 are prod_j f_j(r)

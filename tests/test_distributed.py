@@ -80,7 +80,7 @@ def test_xor_allreduce_gloo():
     mp.spawn(_xor_worker, args=(2, _free_port()), nprocs=2, join=True)
 
 
-def _gpu_worker(rank, world, port, n, d, seed, out_q):
+def _gpu_worker(rank, world, port, n, d, seed, out_q, device_exchange=False):
     """One rank of the world-2 GPU rehearsal: the HIP shard prover (built from this rank's share
     only) driven by ShardedSumcheck over gloo, and this rank's slice of a batched GF(2^128) NTT.
     Both ranks use cuda:0 (the box has one GPU)."""
@@ -99,7 +99,8 @@ def _gpu_worker(rank, world, port, n, d, seed, out_q):
         # this rank's batches b with b mod world == rank, column by column
         share = ev.reshape(d, (1 << n) // 32, 128)[:, rank::world, :]
         t = torch.from_numpy(np.ascontiguousarray(share).reshape(-1).view(np.int32)).to(dev)
-        sc = ShardedSumcheck(B.Sumcheck.from_shard(n, d, t, rank, world))
+        sc = ShardedSumcheck(B.Sumcheck.from_shard(n, d, t, rank, world), device_exchange=device_exchange)
+        assert sc.device_exchange == device_exchange
         sums, pts = [], []
         for r in range(n + 1):
             s, p = sc.this_round_messages()
@@ -125,16 +126,17 @@ def _gpu_worker(rank, world, port, n, d, seed, out_q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,d", [(14, 3), (12, 2)])
-def test_sharded_hip_prover_world2_gloo(n, d, dev):
+@pytest.mark.parametrize("n,d,device_exchange", [(14, 3, False), (12, 2, False), (14, 3, True), (13, 4, True)])
+def test_sharded_hip_prover_world2_gloo(n, d, device_exchange, dev):
     """World-2 gloo run of the HIP shard prover: the all-gathered + XOR-ed transcript equals the
     oracle's unsharded transcript, every rank sees the same messages, and each rank's slice of the
-    batched NTT matches the oracle."""
+    batched NTT matches the oracle. device_exchange=True runs the RCCL path's protocol (message
+    sink, flags, p(1) completed from the global claim) with the sink staged for gloo."""
     import torch.multiprocessing as mp
     seed = 700 + n + d
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    mp.spawn(_gpu_worker, args=(2, _free_port(), n, d, seed, q), nprocs=2, join=True)
+    mp.spawn(_gpu_worker, args=(2, _free_port(), n, d, seed, q, device_exchange), nprocs=2, join=True)
     got = dict()
     for _ in range(2):
         rank, s, p, ok = q.get(timeout=60)
