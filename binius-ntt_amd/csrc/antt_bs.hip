@@ -62,7 +62,11 @@ struct BsParams {
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // streaming (non-temporal) 16-byte global accesses: every byte is touched once per pass
 __device__ __forceinline__ uint4 ld_stream(const uint32_t* p) {
+#ifdef BN_TEMPORAL
+	const u32x4 v = *(const u32x4*)p;
+#else
 	const u32x4 v = __builtin_nontemporal_load((const u32x4*)p);
+#endif
 	return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void st_stream(uint32_t* p, uint4 g) {
@@ -71,7 +75,11 @@ __device__ __forceinline__ void st_stream(uint32_t* p, uint4 g) {
 	v.y = g.y;
 	v.z = g.z;
 	v.w = g.w;
+#ifdef BN_TEMPORAL
+	*(u32x4*)p = v;
+#else
 	__builtin_nontemporal_store(v, (u32x4*)p);
+#endif
 }
 
 // bit masks of the bit-lanes p with bit j of p set
@@ -235,6 +243,9 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 	};
 
 	size_t tile = blockIdx.x;
+#ifdef BN_REV_LAST
+	if (LAST && !PF) tile = P.ntiles - 1 - blockIdx.x;
+#endif
 	geo(tile, outer, outer_off, coset, dst, src);
 	if (PF) issue(src, outer_off);
 	for (;;) {
@@ -982,7 +993,9 @@ const void* bs_pass_kernel(bn_antt_plan* plan, int i) {
 	if (plan->variant == 4 || (plan->variant == 5 && fmax <= 8)) return rr_pass_kernel(plan, pass);
 	if (plan->variant != 1 && plan->variant != 5) return nullptr;
 	const BsDevKnobs kn = dev_knobs();
-	const size_t ntiles = ((size_t)1 << plan->log_rate) << pass.n_outer;  // one transform (bench / profiles)
+	// the kernel for ONE transform (bench / profiles): a batched launch of the same pass may pick
+	// another (the lane-split and prefetching kernels depend on the tile count)
+	const size_t ntiles = ((size_t)1 << plan->log_rate) << pass.n_outer;
 	if (use_split(plan, pass, ntiles, kn)) return split_kernel_for(pass.role);
 	const bool pf = kn.persist && (kn.pf_mode == 2 || (kn.pf_mode == 1 && fmax <= 8));
 	return kernel_for(plan->limbs, pass.role, fmax, pf);

@@ -438,6 +438,9 @@ struct bn_sumcheck {
 	// Round i + 1 then skips point 1 (p(1) = claim + p(0)): (d - 1) fewer products per pair.
 	// The interpolation itself runs in the next round_messages, while its kernel is in flight.
 	bool have_pts = false, have_claim = false, claim_pending = false;
+	// bn_sumcheck_round_messages_sink: the round's points went to the sink unread by the prover; the
+	// caller (the sharded driver) holds the GLOBAL points and completes a skipped p(1) itself
+	bool pts_external = false;
 	uint32_t last_pts[4 * (bn::quad::kMaxD + 1)];
 	uint32_t claim[4], pending_r[4];
 	// move_to_next_round queues the next round's messages kernel right behind the fold, so the
@@ -846,7 +849,7 @@ extern "C" int bn_sumcheck_import_gathered(bn_sumcheck* sc, const uint32_t* word
 	sc->cur = (size_t)32 * world;
 	sc->rank = 0;
 	sc->world = 1;
-	sc->have_pts = sc->have_claim = sc->claim_pending = false;  // the shards' claims are partial: recompute point 1
+	sc->have_pts = sc->have_claim = sc->claim_pending = sc->pts_external = false;  // the shards' claims are partial: recompute point 1
 	sc->msgs_queued = false;
 	return BN_OK;
 }
@@ -877,6 +880,8 @@ extern "C" int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32
 	}
 	sc->msgs_queued = false;
 	int rc = BN_OK;
+	if (sc->claim_pending && sc->pts_external)
+		BN_FAIL(BN_ERR_INVALID, "the previous round's points went to the message sink: read this round there too");
 	if (sc->claim_pending) {  // last round's claim, computed while this round's kernel runs
 		rc = bn_sumcheck_interpolate(sc->last_pts, sc->d + 1, sc->pending_r, sc->claim);
 		if (rc != BN_OK) return rc;
@@ -917,8 +922,33 @@ extern "C" int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32
 		}
 		memcpy(sc->last_pts, points, sizeof(uint32_t) * 4 * npts);
 		sc->have_pts = true;
+		sc->pts_external = false;
 	}
 	sc->have_claim = false;
+	sc->sharded_used = true;
+	return BN_OK;
+}
+
+extern "C" int bn_sumcheck_round_messages_sink(bn_sumcheck* sc) {
+	BN_CHECK_ARG(sc, "NULL prover");
+	BN_CHECK_ARG(sc->sink, "no message sink set (bn_sumcheck_set_message_sink)");
+	BN_CHECK_ARG(!(sc->world > 1 && sc->cur <= 32), "shard exhausted: gather (export_shard/import_gathered) first");
+	DeviceScope ds(sc->device);
+	if (!sc->prepared) {
+		const int prc = sc_prepare(sc);
+		if (prc != BN_OK) return prc;
+	}
+	if (!sc->msgs_queued) {
+		const int rc = queue_messages(sc);
+		if (rc != BN_OK) return rc;
+	}
+	// no poll: the words reach the sink on the prover's stream, where the caller orders its reads.
+	// The caller holds this round's global points, so the next round may skip p(1) (flag bit 0 of
+	// sink word 36 says when it did)
+	sc->msgs_queued = false;
+	sc->claim_pending = sc->have_claim = false;
+	sc->have_pts = sc->cur > 1;
+	sc->pts_external = true;
 	sc->sharded_used = true;
 	return BN_OK;
 }

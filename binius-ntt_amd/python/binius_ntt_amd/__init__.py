@@ -90,6 +90,7 @@ def lib():
         "bn_sumcheck_create_shard_device": (i32, [i32, i32, i32, i32, i32, vp, vp, ctypes.POINTER(vp)]),
         "bn_sumcheck_needs_gather": (i32, [vp, ctypes.POINTER(i32)]),
         "bn_sumcheck_set_message_sink": (i32, [vp, vp]),
+        "bn_sumcheck_round_messages_sink": (i32, [vp]),
         "bn_sumcheck_stream": (i32, [vp, ctypes.POINTER(vp)]),
         "bn_sumcheck_export_shard": (i32, [vp, u32p, sz]),
         "bn_sumcheck_import_gathered": (i32, [vp, u32p, sz, i32]),
@@ -595,6 +596,11 @@ class Sumcheck:
         _check_device_tensor(words, 4 * (8 + 1) + 1, "message sink")
         self._sink = words  # keep the buffer alive while the prover writes it
         _check(lib().bn_sumcheck_set_message_sink(self._sc, _ptr(words)))
+
+    def round_messages_sink(self):
+        """bn_sumcheck_round_messages_sink: the round's messages kernel is queued (no wait); its raw
+        points land in the sink on stream_handle()'s stream."""
+        _check(lib().bn_sumcheck_round_messages_sink(self._sc))
 
     def stream_handle(self):
         """The prover's hipStream_t (as an int), for torch.cuda.ExternalStream."""

@@ -99,17 +99,18 @@ class ShardedSumcheck:
 
     Exchange paths for the per-round (sum, points) words:
       * device (default on an nccl group with a HIP prover): the prover's messages kernel also writes
-        its raw partial points into a preallocated device sink (bn_sumcheck_set_message_sink),
-        `all_gather_into_tensor` reads the sink directly and one copy brings the world x 40 words
-        back; the partial points are XOR-ed and
-        p(1), sum are completed from the GLOBAL claim (p(1) = claim + p(0), sum = claim, the claim
-        being the previous round's global points interpolated at its challenge) — so no
-        numpy -> pinned -> H2D hop per round;
-      * host (gloo, or a prover without a sink): the words the prover returned are staged through
-        WordExchange.
+        its raw partial points into a preallocated device sink (bn_sumcheck_set_message_sink) and
+        the round is read with bn_sumcheck_round_messages_sink, which does not wait for the kernel.
+        `all_gather_into_tensor` of the sink is enqueued on the PROVER's stream right behind the
+        messages kernel, one copy on that stream brings the world x 40 words back, and the host
+        waits only for that copy. The partial points are XOR-ed and p(1), sum are completed from the
+        GLOBAL claim (p(1) = claim + p(0), sum = claim, the claim being the previous round's global
+        points interpolated at its challenge);
+      * host (gloo, or a prover without a sink): the prover's round_messages polls its posted
+        points and the words are staged through WordExchange.
     device_exchange=True on a gloo group keeps the device path's protocol (sink, flags, p(1) from
-    the global claim) and stages only the sink through host memory for the CPU collective: the
-    world-2 gloo GPU test runs the multi-rank device path that way.
+    the global claim) and stages only the sink through host memory (a copy on the prover's stream)
+    for the CPU collective: the world-2 gloo GPU test runs the multi-rank device path that way.
     exchange_at_world1=True runs the exchange even when the group has one rank (the RCCL rehearsal
     on a one-GPU box exercises the device path that way)."""
 
@@ -122,16 +123,24 @@ class ShardedSumcheck:
         self._msg = None  # WordExchange for the (d + 2) x 4 message words, built on first use
         self.exchange_seconds = 0.0  # per-round message exchanges + the endgame gather
         self.exchange_rounds = 0
+        self.round_seconds = 0.0  # whole this_round_messages calls (the round's kernel wait included)
         if device_exchange is None:
             device_exchange = dist.is_initialized() and dist.get_backend(group) == "nccl"
-        self.device_exchange = bool(device_exchange) and hasattr(prover, "set_message_sink") and not self.replicated
+        self.device_exchange = (bool(device_exchange) and hasattr(prover, "round_messages_sink")
+                                and not self.replicated)
         self._claim = None     # global claim of the coming round (device path)
         self._last_pts = None  # previous round's global points (device path)
         if self.device_exchange:
             import torch
             pdev = torch.device("cuda", prover.device if getattr(prover, "device", None) is not None
                                 else torch.cuda.current_device())
-            self._stage = _device_for(dist, group).type != "cuda"  # a CPU collective (gloo)
+            cdev = _device_for(dist, group)
+            self._stage = cdev.type != "cuda"  # a CPU collective (gloo)
+            if not self._stage and cdev != pdev:
+                raise ValueError("ShardedSumcheck: the prover runs on %s but the process group's device is %s"
+                                 % (pdev, cdev))
+            # the prover's own stream: the sink's consumers are enqueued behind its messages kernel
+            self._pstream = torch.cuda.ExternalStream(prover.stream_handle(), device=pdev)
             self._sink = torch.zeros(SINK_WORDS, dtype=torch.int32, device=pdev)
             if self._stage:
                 self._send = torch.empty(SINK_WORDS, dtype=torch.int32)
@@ -157,20 +166,23 @@ class ShardedSumcheck:
         import torch
         import torch.distributed as dist
         t0 = time.perf_counter()
-        # no stream wait: the prover's this_round_messages has already seen the round's posted
-        # sequence number, which the posting workgroup releases at system scope after writing the
-        # sink words, and the collective's kernel is dispatched after that (with the dispatch's
-        # acquire), so it reads the complete words
-        if self._stage:
-            self._send.copy_(self._sink)  # synchronous device -> host
-            dist.all_gather_into_tensor(self._recv, self._send, group=self.group)
-            g = self._recv.numpy().view(np.uint32).reshape(self.world, SINK_WORDS)
-        else:
-            dist.all_gather_into_tensor(self._recv, self._sink, group=self.group)
-            self._h_recv.copy_(self._recv)  # synchronous: the host needs the words now
-            g = self._h_recv.numpy().view(np.uint32).reshape(self.world, SINK_WORDS)
+        self.prover.round_messages_sink()  # queued, not waited for
+        # everything below runs on the prover's stream, behind its messages kernel (the documented
+        # consumer contract of bn_sumcheck_set_message_sink); the host waits only for the last copy
+        with torch.cuda.stream(self._pstream):
+            if self._stage:
+                self._send.copy_(self._sink)  # device -> pageable host: synchronous on this stream
+                dist.all_gather_into_tensor(self._recv, self._send, group=self.group)
+                g = self._recv.numpy().view(np.uint32).reshape(self.world, SINK_WORDS)
+            else:
+                dist.all_gather_into_tensor(self._recv, self._sink, group=self.group)
+                self._h_recv.copy_(self._recv)  # after the collective on this stream; synchronous
+                g = self._h_recv.numpy().view(np.uint32).reshape(self.world, SINK_WORDS)
+        flag_words = g[:, 36]
+        if not np.all(flag_words == flag_words[0]):
+            raise RuntimeError("ShardedSumcheck: ranks disagree on the round's flags %s" % flag_words.tolist())
         raw = np.bitwise_xor.reduce(g[:, :4 * d1], axis=0).reshape(d1, 4).copy()
-        flags = int(g[0, 36])
+        flags = int(flag_words[0])
         if flags & 2:  # the last call (one evaluation left): words 0-3 are prod_j f_j(r)
             s = raw[0].copy()
             raw[:] = 0
@@ -186,16 +198,24 @@ class ShardedSumcheck:
         return s, raw
 
     def this_round_messages(self):
+        import time
+        t0 = time.perf_counter()
+        try:
+            return self._round_messages()
+        finally:
+            self.round_seconds += time.perf_counter() - t0
+
+    def _round_messages(self):
         self._gather_if_needed()
-        s, pts = self.prover.this_round_messages()
-        d1 = pts.shape[0]
         if self.replicated:
             self._last_pts = None
-            return s, pts
+            return self.prover.this_round_messages()
         if self.device_exchange:
-            s, pts = self._device_round(d1)
+            s, pts = self._device_round(self.prover.d + 1)
             self._last_pts = pts
             return s, pts
+        s, pts = self.prover.this_round_messages()
+        d1 = pts.shape[0]
         flat = np.concatenate([np.asarray(s, np.uint32).reshape(-1), np.asarray(pts, np.uint32).reshape(-1)])
         if self._msg is None:
             self._msg = WordExchange(flat.size, self.group)

@@ -217,6 +217,14 @@ int bn_sumcheck_needs_gather(const bn_sumcheck* sc, int* flag);
  * once bn_sumcheck_round_messages has returned; consumers on other streams order themselves after
  * the prover's stream (bn_sumcheck_stream) to read them. */
 int bn_sumcheck_set_message_sink(bn_sumcheck* sc, void* d_words);
+/* Sharded drivers with a message sink: replaces bn_sumcheck_round_messages without waiting for the
+ * round. Makes sure the round's messages kernel is queued on the prover's stream and returns; the
+ * raw points and flags reach the sink in stream order, so a consumer orders itself after
+ * bn_sumcheck_stream (e.g. enqueues its collective there) and never polls the host. The caller
+ * then holds the round's global points: the next round skips p(1) when the prover derives it
+ * (sink word 36 bit 0) and the caller completes it from the global claim. Once used, the rounds
+ * up to the endgame gather must all be read this way. */
+int bn_sumcheck_round_messages_sink(bn_sumcheck* sc);
 int bn_sumcheck_stream(const bn_sumcheck* sc, void** stream);
 int bn_sumcheck_export_shard(const bn_sumcheck* sc, uint32_t* out, size_t out_words);
 int bn_sumcheck_import_gathered(bn_sumcheck* sc, const uint32_t* words, size_t n_words, int world);

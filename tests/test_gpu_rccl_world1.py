@@ -57,19 +57,29 @@ SCRIPT = textwrap.dedent("""
     ref = B.Sumcheck(n, d, True, ev)
     want = transcript(ref)
     ref.close()
-    stats = {}
-    for mode in ("device", "host"):
-        pr = B.Sumcheck(n, d, True, ev)
-        sc = D.ShardedSumcheck(pr, device_exchange=(mode == "device"), exchange_at_world1=True)
-        assert sc.device_exchange == (mode == "device")
-        got = transcript(sc)
-        for r, ((s1, p1), (s2, p2)) in enumerate(zip(got, want)):
-            assert np.array_equal(s1, s2) and np.array_equal(p1, p2), (mode, r)
-        assert sc.exchange_rounds == n + 1
-        stats[mode + "_exchange_ms_per_round"] = sc.exchange_seconds * 1e3 / sc.exchange_rounds
-        pr.close()
+    # per-round cost of each path: whole transcripts (round kernels, waits and exchanges), the
+    # modes alternated over several repetitions after one warm-up transcript each
+    stats = {"device_round_ms": [], "host_round_ms": [], "device_exchange_ms": [], "host_exchange_ms": []}
+    for rep in range(4):
+        for mode in ("device", "host"):
+            pr = B.Sumcheck(n, d, True, ev)
+            sc = D.ShardedSumcheck(pr, device_exchange=(mode == "device"), exchange_at_world1=True)
+            assert sc.device_exchange == (mode == "device")
+            t0 = time.perf_counter()
+            got = transcript(sc)
+            dt = time.perf_counter() - t0
+            for r, ((s1, p1), (s2, p2)) in enumerate(zip(got, want)):
+                assert np.array_equal(s1, s2) and np.array_equal(p1, p2), (mode, r)
+            assert sc.exchange_rounds == n + 1
+            if rep:
+                stats[mode + "_round_ms"].append(dt * 1e3 / (n + 1))
+                stats[mode + "_exchange_ms"].append(sc.round_seconds * 1e3 / (n + 1))
+            pr.close()
+    stats = {k: float(np.median(v)) for k, v in stats.items()}
     dist.destroy_process_group()
-    print("EXCHANGE " + json.dumps(dict(stats, n=n, d=d, world=1, backend="nccl")))
+    print("EXCHANGE " + json.dumps(dict(stats, n=n, d=d, world=1, backend="nccl",
+                                        note="round_ms: transcript wall time per round; exchange_ms: "
+                                             "this_round_messages per round (kernel wait included)")))
     print("rccl world1 ok")
 """)
 
