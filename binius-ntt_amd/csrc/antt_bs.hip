@@ -62,11 +62,7 @@ struct BsParams {
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // streaming (non-temporal) 16-byte global accesses: every byte is touched once per pass
 __device__ __forceinline__ uint4 ld_stream(const uint32_t* p) {
-#ifdef BN_TEMPORAL
-	const u32x4 v = *(const u32x4*)p;
-#else
 	const u32x4 v = __builtin_nontemporal_load((const u32x4*)p);
-#endif
 	return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void st_stream(uint32_t* p, uint4 g) {
@@ -75,11 +71,7 @@ __device__ __forceinline__ void st_stream(uint32_t* p, uint4 g) {
 	v.y = g.y;
 	v.z = g.z;
 	v.w = g.w;
-#ifdef BN_TEMPORAL
-	*(u32x4*)p = v;
-#else
 	__builtin_nontemporal_store(v, (u32x4*)p);
-#endif
 }
 
 // bit masks of the bit-lanes p with bit j of p set
@@ -243,9 +235,6 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 	};
 
 	size_t tile = blockIdx.x;
-#ifdef BN_REV_LAST
-	if (LAST && !PF) tile = P.ntiles - 1 - blockIdx.x;
-#endif
 	geo(tile, outer, outer_off, coset, dst, src);
 	if (PF) issue(src, outer_off);
 	for (;;) {
