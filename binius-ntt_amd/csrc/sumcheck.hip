@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -392,6 +393,210 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_coal(ScArgs A) {
 	}
 }
 
+// ---------------------------------------------------------------------------------------
+// Round server for the last rounds (at most kServerMaxCur evaluations per column left): ONE
+// resident 512-thread workgroup runs every remaining round by itself. It waits for the host's
+// challenge in host-mapped control words, folds, computes the next round's messages on 16-lane
+// products and posts them exactly as sc_messages does (points, then the sequence word). A small
+// round then costs no kernel launch, no dispatch ramp and no cross-workgroup reduction: with one
+// fold and one messages launch per round the last rounds of c4 took ~10 us (fold) + ~18 us
+// (messages) of kernel time plus ~12 us of host launches each (round-4 trace).
+// A waiting server holds its hardware queue, and work that other streams of the process queue
+// behind it on the same queue (HIP maps streams onto a few queues) waits too. So the wait is short
+// (kSrvTimeoutTicks of s_memrealtime): a server that gets no challenge in time records the last
+// ticket it served (kCtlExit) and ends, and the host relaunches one when it next needs it
+// (bn_sumcheck_round_messages). bn_sumcheck_destroy posts kSrvStop.
+// ---------------------------------------------------------------------------------------
+constexpr int kSrvThreads = 768;  // 12 waves: three per SIMD (the wide product fits 168 VGPRs)
+constexpr int kSrvG = 64;  // wide_mul: latency is all that counts here (a few items per round)
+constexpr int kSrvGroups = kSrvThreads / kSrvG;
+#ifndef BN_SC_SERVER_MAX
+#define BN_SC_SERVER_MAX 512
+#endif
+constexpr size_t kServerMaxCur = BN_SC_SERVER_MAX;  // (-DBN_SC_SERVER_MAX=0: no server, A/B builds)
+constexpr uint32_t kSrvStop = 0xFFFFFFFFu;
+constexpr int kCtlR = 0, kCtlSkip = 4, kCtlTicket = 5, kCtlExit = 6, kCtlWords = 8;  // host-mapped control words
+constexpr uint32_t kSrvRunning = 0xFFFFFFFEu;                   // kCtlExit while a server may be alive
+constexpr unsigned long long kSrvTimeoutTicks = 20000ull;        // 200 us at 100 MHz
+
+struct SrvArgs {
+	uint32_t* cols;
+	size_t col_stride;
+	int d;
+	size_t cur;           // evaluations per column before the first fold
+	uint32_t* res;        // host-mapped points + sequence word (as ScArgs::res)
+	const uint32_t* ctl;  // host-mapped control words: challenge, skip-p(1) flag, ticket
+	uint32_t* ctl_exit;   // ... kCtlExit: the last ticket served by a server that timed out
+	uint32_t seq;         // sequence number of the first posted round
+	uint32_t ticket;      // ticket of the first challenge
+	uint32_t kcol[kMaxD + 1][4];
+	unsigned long long* trace;  // development build: per round, s_memrealtime at wake, fold, messages, post
+};
+
+template <int MODE>
+__device__ __forceinline__ void srv_fold(const ScArgs& a, const Slot& S, const uint32_t* R, int qw, int l) {
+	const size_t items = (size_t)a.d * a.n_pairs;
+	for (size_t it = qw; it < items; it += kSrvGroups) {
+		const int j = (int)(it / a.n_pairs);
+		const size_t p = it % a.n_pairs;
+		uint32_t lo[32], hi[32], emask = 0;
+		if (l < 4) {
+			load_pair<MODE>(a, j, p, l, lo, hi, emask);
+#pragma unroll
+			for (int i = 0; i < 32; i++) hi[i] ^= lo[i];
+			sst(S, l, hi);
+		}
+		grp_mul<kSrvG, true>(S, R, l);
+		if (l < 4) {
+			sld(hi, S, l);
+			uint32_t* o = a.cols + (size_t)j * a.col_stride + (MODE == 0 ? 128 * p : 0) + 32 * l;
+			if (MODE == 0) {
+#pragma unroll
+				for (int i = 0; i < 32; i++) lo[i] ^= hi[i];
+			} else {
+				// in-batch pairs: the folded values replace the low half's bit-lanes
+#pragma unroll
+				for (int i = 0; i < 32; i++) lo[i] = (lo[i] ^ hi[i]) & emask;
+			}
+			st32(o, lo);
+		}
+		wsync();
+	}
+}
+
+template <int MODE>
+__device__ __forceinline__ void srv_messages(const ScArgs& a, const uint32_t (*kcol)[4], const Slot& S, uint32_t* accL, int qw,
+                                             int l) {
+	const int npts = a.kmax + 1 - a.skip1;
+	const size_t items = a.n_pairs * (size_t)npts;
+	for (size_t item = qw; item < items; item += kSrvGroups) {
+		const size_t p = item / npts;
+		const int ki = (int)(item % npts);
+		const int k = (a.skip1 && ki >= 1) ? ki + 1 : ki;
+		uint32_t emask = 0;
+		for (int j = 0; j < a.d; j++) {
+			if (l < 4) {
+				uint32_t lo[32], hi[32];
+				load_pair<MODE>(a, j, p, l, lo, hi, emask);
+				if (k == 1) {
+#pragma unroll
+					for (int i = 0; i < 32; i++) lo[i] = hi[i];
+				} else if (k > 1) {
+#pragma unroll
+					for (int i = 0; i < 32; i++) hi[i] ^= lo[i];
+					if (a.kmax <= 3)
+						mul_23(0u - (uint32_t)(k & 1), hi);
+					else
+						mul_small(kcol[k], hi, hi);
+#pragma unroll
+					for (int i = 0; i < 32; i++) lo[i] ^= hi[i];
+				}
+				sst(S, (j == 0 ? 0 : 4) + l, lo);
+			}
+			if (j > 0) grp_mul<kSrvG, false>(S, nullptr, l);
+		}
+		wsync();
+		if (l < 4) {
+			uint32_t t[32];
+			sld(t, S, l);
+			const uint32_t acc = parity_word(t, emask);
+			if (acc) atomicXor(accL + 4 * k + l, acc);
+		}
+		wsync();
+	}
+}
+
+__global__ __launch_bounds__(kSrvThreads, 1) void sc_server(SrvArgs P) {
+	extern __shared__ uint32_t lds[];
+	const int l = threadIdx.x % kSrvG, qw = threadIdx.x / kSrvG;
+	const Slot S{lds + qw * Grp<kSrvG>::kSlotWords};
+	uint32_t* R = lds + kSrvGroups * Grp<kSrvG>::kSlotWords;  // the challenge, broadcast-bitsliced
+	uint32_t* accL = R + 128;                    // (kMaxD + 1) x 4 point words
+	uint32_t* ctlL = accL + 4 * (kMaxD + 1);     // [0] wake-up reason, [1] skip-p(1) flag
+	ScArgs a{};
+	a.cols = P.cols;
+	a.col_stride = P.col_stride;
+	a.d = P.d;
+	size_t cur = P.cur;
+	uint32_t seq = P.seq, ticket = P.ticket;
+	for (;;) {
+		// ---- the host's challenge for the fold of this round
+		if (threadIdx.x == 0) {
+			const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+			uint32_t why = 2;  // timed out
+			for (;;) {
+				const uint32_t t = __hip_atomic_load(P.ctl + kCtlTicket, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+				if (t == ticket) { why = 0; break; }
+				if (t == kSrvStop) { why = 1; break; }
+				if (__builtin_amdgcn_s_memrealtime() - t0 > kSrvTimeoutTicks) break;
+				__builtin_amdgcn_s_sleep(2);
+			}
+			ctlL[0] = why;
+			ctlL[1] = __hip_atomic_load(P.ctl + kCtlSkip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+		}
+		__syncthreads();
+#ifdef BN_DEV
+		unsigned long long* trw = P.trace ? P.trace + 4 * (size_t)(ticket % 64) : nullptr;
+		if (trw && threadIdx.x == 0) trw[0] = __builtin_amdgcn_s_memrealtime();
+#endif
+		if (ctlL[0] != 0) {
+			// timed out: tell the host which ticket was served last (it relaunches for the next)
+			if (ctlL[0] == 2 && threadIdx.x == 0)
+				__hip_atomic_store(P.ctl_exit, ticket - 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+			return;
+		}
+		if (threadIdx.x < 128) {
+			const uint32_t rw = __hip_atomic_load(P.ctl + kCtlR + threadIdx.x / 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			R[threadIdx.x] = 0u - ((rw >> (threadIdx.x % 32)) & 1u);
+		}
+		if (threadIdx.x < 4 * (kMaxD + 1)) accL[threadIdx.x] = 0;
+		__syncthreads();
+		// ---- fold: cur -> cur / 2
+		a.n_pairs = cur >= 64 ? cur / 64 : 1;
+		a.hb = cur / 64;
+		a.h = (int)(cur / 2);
+		if (cur >= 64)
+			srv_fold<0>(a, S, R, qw, l);
+		else
+			srv_fold<1>(a, S, R, qw, l);
+		cur /= 2;
+		__syncthreads();  // every folded column word is written (one CU: the workgroup's fence suffices)
+#ifdef BN_DEV
+		if (trw && threadIdx.x == 0) trw[1] = __builtin_amdgcn_s_memrealtime();
+#endif
+		// ---- the next round's messages
+		const int mode = cur >= 64 ? 0 : cur >= 2 ? 1 : 2;
+		a.mode = mode;
+		a.n_pairs = cur >= 64 ? cur / 64 : 1;
+		a.hb = cur / 64;
+		a.h = (int)(cur / 2);
+		a.kmax = mode == 2 ? 0 : a.d;
+		a.skip1 = mode == 2 ? 0 : (int)(ctlL[1] & 1u);
+		if (mode == 0)
+			srv_messages<0>(a, P.kcol, S, accL, qw, l);
+		else if (mode == 1)
+			srv_messages<1>(a, P.kcol, S, accL, qw, l);
+		else
+			srv_messages<2>(a, P.kcol, S, accL, qw, l);
+		__syncthreads();
+#ifdef BN_DEV
+		if (trw && threadIdx.x == 0) trw[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+		if (threadIdx.x < 4 * (a.kmax + 1)) P.res[threadIdx.x] = accL[threadIdx.x];
+		__threadfence_system();
+		__syncthreads();
+#ifdef BN_DEV
+		if (trw && threadIdx.x == 0) trw[3] = __builtin_amdgcn_s_memrealtime();
+#endif
+		if (threadIdx.x == 0) __hip_atomic_store(P.res + kResSeq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+		if (cur == 1) return;  // the final evaluation is posted: no fold left
+		seq++;
+		ticket++;
+	}
+}
+
+size_t srv_lds_bytes() { return ((size_t)kSrvGroups * Grp<kSrvG>::kSlotWords + 128 + 4 * (kMaxD + 1) + 2) * sizeof(uint32_t); }
+
 // quad slots + the fold's broadcast challenge (128 words) + the messages' accumulators, flag and
 // last-workgroup reduction
 template <int G>
@@ -450,6 +655,15 @@ struct bn_sumcheck {
 	// the sum from the data instead of deriving them from the claim, so the verifier's
 	// p(0) + p(1) == previous p(r) check also tests the folds (tests/test_gpu_sumcheck.py)
 	bool derive_p1 = !(getenv("BN_SUMCHECK_FULL_POINTS") && atoi(getenv("BN_SUMCHECK_FULL_POINTS")) != 0);
+	// round server (sc_server) for the last rounds: running once launched until cur == 1
+	uint32_t* h_ctl = nullptr;  // host-mapped control words (challenge, skip flag, ticket)
+	bool server = false;
+	uint32_t ticket = 0;
+	size_t server_max_cur = bn::kServerMaxCur;  // BN_SC_SERVER_MAX_CUR (development build) overrides
+	uint32_t last_sum[4] = {0, 0, 0, 0}, last_points[4 * (bn::quad::kMaxD + 1)];  // the round read last
+	unsigned long long* h_trace = nullptr;  // development build (BN_SC_TIMING): the server's phase stamps
+	double t_post = 0;                      // ... and the host's time of the last challenge post
+	bool read_this_round = false;
 };
 
 namespace {
@@ -533,6 +747,101 @@ int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 	return BN_OK;
 }
 
+#ifdef BN_DEV
+double host_us() {
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+#endif
+
+// The round server takes over once at most server_max_cur evaluations per column are left (an
+// unsharded, eager prover without a message sink; composition_eval only folds)
+bool server_eligible(const bn_sumcheck* sc) {
+	return sc->eager && sc->world == 1 && !sc->sink && sc->prepared && sc->cur >= 2 && sc->cur <= sc->server_max_cur;
+}
+
+// a server that folds `cur` evaluations per column on `ticket` and posts those messages as `seq`
+int server_launch(bn_sumcheck* sc, size_t cur, uint32_t seq, uint32_t ticket) {
+	SrvArgs P{};
+	P.cols = sc->cols;
+	P.col_stride = sc->col_words;
+	P.d = sc->d;
+	P.cur = cur;
+	P.res = sc->d_res;
+	uint32_t* d_ctl = nullptr;
+	BN_HIP(hipHostGetDevicePointer((void**)&d_ctl, sc->h_ctl, 0));
+	P.ctl = d_ctl;
+	P.ctl_exit = d_ctl + kCtlExit;
+	P.seq = seq;
+	P.ticket = ticket;
+	P.trace = nullptr;
+#ifdef BN_DEV
+	if (getenv("BN_SC_TIMING")) {
+		if (!sc->h_trace) {
+			BN_HIP(hipHostMalloc((void**)&sc->h_trace, 64 * 4 * sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent));
+			memset(sc->h_trace, 0, 64 * 4 * sizeof(unsigned long long));
+		}
+		BN_HIP(hipHostGetDevicePointer((void**)&P.trace, sc->h_trace, 0));
+	}
+#endif
+	((volatile uint32_t*)sc->h_ctl)[kCtlExit] = kSrvRunning;
+	for (int k = 0; k <= kMaxD; k++)
+		for (int a = 0; a < 4; a++) P.kcol[k][a] = (uint32_t)tw_mul((uint64_t)k, 1ull << a, 2);
+	void* args[] = {&P};
+	BN_HIP(hipLaunchKernel((const void*)sc_server, dim3(1), dim3(kSrvThreads), args, srv_lds_bytes(), sc->stream));
+	sc->server = true;
+	return BN_OK;
+}
+
+// hand the server its next challenge (the fold of this round, then the next round's messages)
+void server_post(bn_sumcheck* sc, const uint32_t* r, bool skip1) {
+	volatile uint32_t* c = sc->h_ctl;
+	for (int i = 0; i < 4; i++) c[kCtlR + i] = r[i];
+	c[kCtlSkip] = skip1 ? 1u : 0u;
+	std::atomic_thread_fence(std::memory_order_release);
+	c[kCtlTicket] = ++sc->ticket;
+	sc->seq++;  // the server posts this round's messages with the next sequence number
+#ifdef BN_DEV
+	sc->t_post = host_us();
+#endif
+}
+
+// Wait for the round's posted sequence number (the stream is queried between polls, so a failed
+// kernel is reported rather than waited for); relaunches a round server that timed out before
+// taking this round's challenge.
+int wait_posted(bn_sumcheck* sc) {
+	const volatile uint32_t* posted = sc->h_res + kResSeq;
+	for (;;) {
+		bool seen = false;
+		for (int i = 0; i < 4096 && !(seen = *posted == sc->seq); i++) {
+		}
+		if (seen) {
+#ifdef BN_DEV
+			if (sc->server && sc->h_trace && sc->ticket > 0) {
+				const unsigned long long* t = sc->h_trace + 4 * (size_t)(sc->ticket % 64);
+				fprintf(stderr, "server round cur=%zu: post->seen %.1f us | wake->fold %.1f fold->msgs %.1f msgs->post %.1f us\n", sc->cur,
+				        host_us() - sc->t_post, (t[1] - t[0]) / 100.0, (t[2] - t[1]) / 100.0, (t[3] - t[2]) / 100.0);
+			}
+#endif
+			return BN_OK;
+		}
+		if (sc->server && ((volatile uint32_t*)sc->h_ctl)[kCtlExit] == sc->ticket - 1) {
+			// the challenge and the ticket are already posted: the new server folds 2 cur down to cur
+			std::atomic_thread_fence(std::memory_order_acquire);
+			const int lrc = server_launch(sc, sc->cur * 2, sc->seq, sc->ticket);
+			if (lrc != BN_OK) return lrc;
+			continue;
+		}
+		const hipError_t e = hipStreamQuery(sc->stream);
+		if (e == hipSuccess) {
+			if (*posted == sc->seq) return BN_OK;
+			BN_FAIL(BN_ERR_HIP, "round messages were not posted (sequence %u)", sc->seq);
+		}
+		if (e != hipErrorNotReady) BN_FAIL(BN_ERR_HIP, "round messages kernel: %s", hipGetErrorString(e));
+	}
+}
+
 int queue_messages(bn_sumcheck* sc) {
 	int rc = sc_launch(sc, false, nullptr);
 	if (rc != BN_OK) return rc;
@@ -554,6 +863,12 @@ int sc_common_init(bn_sumcheck* sc) {
 	BN_HIP(hipHostMalloc((void**)&sc->h_res, sizeof(uint32_t) * (kResSeq + 1), hipHostMallocMapped | hipHostMallocCoherent));
 	memset(sc->h_res, 0, sizeof(uint32_t) * (kResSeq + 1));
 	BN_HIP(hipHostGetDevicePointer((void**)&sc->d_res, sc->h_res, 0));
+	BN_HIP(hipHostMalloc((void**)&sc->h_ctl, sizeof(uint32_t) * kCtlWords, hipHostMallocMapped | hipHostMallocCoherent));
+	memset(sc->h_ctl, 0, sizeof(uint32_t) * kCtlWords);
+	BN_HIP(hipFuncSetAttribute((const void*)sc_server, hipFuncAttributeMaxDynamicSharedMemorySize, (int)srv_lds_bytes()));
+#ifdef BN_DEV
+	if (const char* e = getenv("BN_SC_SERVER_MAX_CUR")) sc->server_max_cur = (size_t)atol(e);
+#endif
 	const void* fns[16] = {(const void*)sc_messages<0, 4>,  (const void*)sc_messages<1, 4>,  (const void*)sc_messages<2, 4>,
 						   (const void*)sc_fold<0, 4>,      (const void*)sc_fold<1, 4>,      (const void*)sc_fold<2, 4>,
 						   (const void*)sc_messages<0, 16>, (const void*)sc_messages<1, 16>, (const void*)sc_messages<2, 16>,
@@ -567,10 +882,16 @@ int sc_common_init(bn_sumcheck* sc) {
 
 void sc_free(bn_sumcheck* sc) {
 	if (!sc) return;
+	if (sc->server && sc->h_ctl) {  // a server still waiting for a challenge: release it
+		std::atomic_thread_fence(std::memory_order_release);
+		((volatile uint32_t*)sc->h_ctl)[kCtlTicket] = kSrvStop;
+	}
 	if (sc->stream) (void)hipStreamSynchronize(sc->stream);
 	if (sc->cols) (void)hipFree(sc->cols);
 	if (sc->acc) (void)hipFree(sc->acc);
 	if (sc->h_res) (void)hipHostFree(sc->h_res);
+	if (sc->h_ctl) (void)hipHostFree(sc->h_ctl);
+	if (sc->h_trace) (void)hipHostFree(sc->h_trace);
 	if (sc->stream) (void)hipStreamDestroy(sc->stream);
 	delete sc;
 }
@@ -874,6 +1195,14 @@ extern "C" int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32
 		const int prc = sc_prepare(sc);
 		if (prc != BN_OK) return prc;
 	}
+	if (!sc->msgs_queued && sc->server) {
+		// this round was read already and the server is waiting for the next challenge (no launch
+		// may queue behind it): the same messages again
+		if (!sc->read_this_round) BN_FAIL(BN_ERR_INVALID, "round server: no messages for this round");
+		memcpy(sum, sc->last_sum, 16);
+		memcpy(points, sc->last_points, sizeof(uint32_t) * 4 * (sc->d + 1));
+		return BN_OK;
+	}
 	if (!sc->msgs_queued) {
 		int rc = queue_messages(sc);
 		if (rc != BN_OK) return rc;
@@ -888,21 +1217,7 @@ extern "C" int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32
 		sc->claim_pending = false;
 		sc->have_claim = sc->cur > 1;
 	}
-	// wait for the posted sequence number (the stream is queried between polls, so a failed
-	// kernel is reported rather than waited for)
-	const volatile uint32_t* posted = sc->h_res + kResSeq;
-	for (;;) {
-		bool seen = false;
-		for (int i = 0; i < 4096 && !(seen = *posted == sc->seq); i++) {
-		}
-		if (seen) break;
-		const hipError_t e = hipStreamQuery(sc->stream);
-		if (e == hipSuccess) {
-			if (*posted == sc->seq) break;
-			BN_FAIL(BN_ERR_HIP, "round messages were not posted (sequence %u)", sc->seq);
-		}
-		if (e != hipErrorNotReady) BN_FAIL(BN_ERR_HIP, "round messages kernel: %s", hipGetErrorString(e));
-	}
+	if ((rc = wait_posted(sc)) != BN_OK) return rc;
 	std::atomic_thread_fence(std::memory_order_acquire);
 	const int npts = sc->d + 1;
 	uint32_t acc[4 * (kMaxD + 1)];
@@ -926,6 +1241,9 @@ extern "C" int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32
 	}
 	sc->have_claim = false;
 	sc->sharded_used = true;
+	memcpy(sc->last_sum, sum, 16);
+	memcpy(sc->last_points, points, sizeof(uint32_t) * 4 * npts);
+	sc->read_this_round = true;
 	return BN_OK;
 }
 
@@ -962,13 +1280,37 @@ extern "C" int bn_sumcheck_move_to_next_round(bn_sumcheck* sc, const uint32_t* c
 		const int prc = sc_prepare(sc);
 		if (prc != BN_OK) return prc;
 	}
-	int rc = sc_launch(sc, true, challenge);
-	if (rc != BN_OK) return rc;
+	const bool to_server = sc->server || server_eligible(sc);
+	if (!to_server) {
+		int rc = sc_launch(sc, true, challenge);
+		if (rc != BN_OK) return rc;
+	}
 	// no sync: the fold is ordered before the next round's messages on the prover's stream
 	sc->have_claim = false;  // a claim not consumed by this round's messages is stale now
 	sc->claim_pending = sc->have_pts && sc->derive_p1;
 	if (sc->claim_pending) memcpy(sc->pending_r, challenge, 16);
 	sc->have_pts = false;
+	sc->read_this_round = false;
+	if (to_server) {
+		// the round server folds and computes the next round's messages (p(1) skipped when the
+		// claim is derived; never for the final evaluation, which the server decides itself)
+		if (sc->server && sc->msgs_queued) {
+			// the previous challenge's messages were not read: let them land first (one ticket at a
+			// time, so a relaunched server never misses an overwritten challenge)
+			const int wrc = wait_posted(sc);
+			if (wrc != BN_OK) return wrc;
+		}
+		if (!sc->server || ((volatile uint32_t*)sc->h_ctl)[kCtlExit] == sc->ticket) {
+			const int rc = server_launch(sc, sc->cur, sc->seq + 1, sc->ticket + 1);
+			if (rc != BN_OK) return rc;
+		}
+		server_post(sc, challenge, sc->claim_pending && sc->cur / 2 >= 2);
+		sc->cur /= 2;
+		sc->round++;
+		sc->sharded_used = true;
+		sc->msgs_queued = true;
+		return BN_OK;
+	}
 	sc->cur /= 2;
 	sc->round++;
 	sc->sharded_used = true;
