@@ -193,6 +193,20 @@ def kernel_counters(name):
     return None, "kernel %s not in %s" % (name, PMC_FILE)
 
 
+def limiter_of(valu, hbm_frac, ctr):
+    """What bounds the dominant pass, from its committed counters: VALU issue when its VALU
+    instruction rate is a larger fraction of the bitop3 issue ceiling than its algorithmic bytes are
+    of the HBM peak, HBM otherwise; with the share of wave time parked on s_waitcnt (SQ_WAIT_ANY)."""
+    v = valu.get("bitop3_ceiling_frac") if valu else None
+    if v is None:
+        return {"limiter": None, "why": "no PMC counters of this library build (%s)" % (valu or {}).get("note")}
+    out = {"limiter": "valu-issue" if v >= hbm_frac else "hbm",
+           "why": "VALU at %.2f of the bitop3 issue ceiling vs algorithmic HBM bytes at %.2f of peak" % (v, hbm_frac)}
+    if ctr and ctr.get("SQ_WAVE_CYCLES") and ctr.get("SQ_WAIT_ANY") is not None:
+        out["wait_share"] = ctr["SQ_WAIT_ANY"] / ctr["SQ_WAVE_CYCLES"]
+    return out
+
+
 def c5_sumcheck(a, B, D, torch, dev, local, rank, world, backend, barrier, max_over_ranks):
     """Config 5's 2^28-evaluation d = 3 sumcheck, sharded by 32-element batch over the ranks, with the
     per-round all-gather + XOR exchange (distributed.ShardedSumcheck); medians over a.sc_runs."""
@@ -449,8 +463,10 @@ def main():
                 "pass_ms_source": "each pass launched back to back between two hipEvents (bn_antt_time_passes)",
                 "pass_ms_inloop": pass_ms_inloop,
                 "transform_frac": transform_gbps / HBM_PEAK_GBPS,
-                # the pass kernels are VALU-issue bound
-                "limiter": "valu-issue",
+                "limiter": limiter_of(valu, achieved / HBM_PEAK_GBPS, ctr),
+                "duration_note": "kernel_ms / pass_ms are uninstrumented hipEvent timings; the rocprofv3 "
+                                 "kernel traces committed under profiles/ run ~6-9 %% longer per launch "
+                                 "(profiler overhead), so frac recomputed from them is lower by that much",
             },
             "valu": valu,
         }

@@ -327,9 +327,14 @@ static const void* pass_r_fn(int role, int m) {
 	return r[role][m - 6];
 }
 
-// the register variant where it applies (roles 0/1, m in 6..9); BN_BB_LDS=1 forces bb_pass (A/B)
+// the register variant where it applies (roles 0/1, m in 6..9); in the development build BN_BB_LDS=1
+// forces bb_pass (A/B)
 static const void* pass_fn_for(const BbPass& p) {
+#ifdef BN_DEV
 	static const bool lds_only = getenv("BN_BB_LDS") != nullptr;
+#else
+	constexpr bool lds_only = false;
+#endif
 	if (!lds_only && p.role != 2 && p.m >= 6 && p.m <= 9) return pass_r_fn(p.role, p.m);
 	return p.role == 0 ? pass_fn<0>() : p.role == 1 ? pass_fn<1>() : pass_fn<2>();
 }

@@ -30,7 +30,7 @@ struct bn_qm31_sumcheck {
 	unsigned long long* h_acc = nullptr;  // pinned
 	hipStream_t stream = nullptr;
 	int cus = 256;
-	int wg_per_cu = 8;  // grid cap (BN_QM_WG_PER_CU overrides, for tuning)
+	int wg_per_cu = 8;  // grid cap (BN_QM_WG_PER_CU overrides it in the development build, for tuning)
 	int par = 0;  // accumulator set of the next round_messages
 	bool pending = false;  // a fold(r) not yet applied to cols (fused into the next round's messages)
 	uint4 pend_r = {0, 0, 0, 0};
@@ -228,7 +228,9 @@ extern "C" int bn_qm31_sumcheck_create(int device, int num_vars, const uint32_t*
 	int cus = 0;
 	if (e == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
 		S->cus = std::max(cus, 1);
-	if (const char* v = getenv("BN_QM_WG_PER_CU")) S->wg_per_cu = std::max(1, atoi(v));
+#ifdef BN_DEV
+	if (const char* v = getenv("BN_QM_WG_PER_CU")) S->wg_per_cu = std::max(1, atoi(v));  // tuning, development build only
+#endif
 	if (e == hipSuccess) {
 		// QM31(uint32_t) assumes values < p; reduce whatever was passed
 		hipLaunchKernelGGL(qm_reduce, dim3(grid_for(S, words)), dim3(kT), 0, S->stream, S->cols, words);

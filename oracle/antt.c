@@ -214,6 +214,9 @@ static struct {
 	pthread_barrier_t bar;
 	int bar_n;           /* participants the stage barrier is set up for (0: none) */
 } pool = {.mu = PTHREAD_MUTEX_INITIALIZER, .start = PTHREAD_COND_INITIALIZER, .done = PTHREAD_COND_INITIALIZER};
+/* held for a whole orc_antt128_limbwise_mt call: concurrent callers (ctypes releases the GIL) take
+ * turns instead of overwriting each other's job */
+static pthread_mutex_t pool_call = PTHREAD_MUTEX_INITIALIZER;
 
 static void mt_run(const mt_job* a, int id) {
 	const size_t n = (size_t)1 << a->log_h;
@@ -276,14 +279,18 @@ void orc_antt128_limbwise_mt(const uint32_t* in, uint32_t* out, int log_h, int l
 	uint32_t* s = (uint32_t*)calloc((size_t)log_h * (size_t)(width > 0 ? width : 1), sizeof(uint32_t));
 	orc_subspace_evals32(log_h, log_rate, s);
 	const size_t n = (size_t)1 << log_h;
+	pthread_mutex_lock(&pool_call);
 	pthread_mutex_lock(&pool.mu);
 	if (pool.size == 0) pool.size = 1;  /* the caller is thread 0 */
 	while (pool.size < nthreads) {
-		pthread_create(&pool.th[pool.size], NULL, pool_worker, (void*)(intptr_t)pool.size);
+		/* a thread that cannot be created caps this call's participants (no stage barrier ever
+		 * waits for a worker that does not exist) */
+		if (pthread_create(&pool.th[pool.size], NULL, pool_worker, (void*)(intptr_t)pool.size) != 0) break;
 		pool.size++;
 	}
+	if (nthreads > pool.size) nthreads = pool.size;
 	if (nthreads > 1 && pool.bar_n != nthreads) {
-		/* no job is running (calls are serialised by the caller), so the barrier is idle */
+		/* no job is running (pool_call serialises the calls), so the barrier is idle */
 		if (pool.bar_n) pthread_barrier_destroy(&pool.bar);
 		pthread_barrier_init(&pool.bar, NULL, (unsigned)nthreads);
 		pool.bar_n = nthreads;
@@ -309,5 +316,6 @@ void orc_antt128_limbwise_mt(const uint32_t* in, uint32_t* out, int log_h, int l
 			pthread_mutex_unlock(&pool.mu);
 		}
 	}
+	pthread_mutex_unlock(&pool_call);
 	free(s);
 }

@@ -80,10 +80,13 @@ def test_xor_allreduce_gloo():
     mp.spawn(_xor_worker, args=(2, _free_port()), nprocs=2, join=True)
 
 
-def _gpu_worker(rank, world, port, n, d, seed, out_q, device_exchange=False):
+def _gpu_worker(rank, world, port, n, d, seed, out_q, device_exchange=False, busy_stream=False):
     """One rank of the world-2 GPU rehearsal: the HIP shard prover (built from this rank's share
     only) driven by ShardedSumcheck over gloo, and this rank's slice of a batched GF(2^128) NTT.
-    Both ranks use cuda:0 (the box has one GPU)."""
+    Both ranks use cuda:0 (the box has one GPU). busy_stream=True queues unrelated kernels on the
+    prover's own stream between the protocol calls and, every other round, makes the host wait for
+    them: the exchange (enqueued on that stream) and the last rounds' round server (resident on it)
+    must neither deadlock nor reorder the transcript."""
     import torch
     import torch.distributed as dist
 
@@ -101,11 +104,22 @@ def _gpu_worker(rank, world, port, n, d, seed, out_q, device_exchange=False):
         t = torch.from_numpy(np.ascontiguousarray(share).reshape(-1).view(np.int32)).to(dev)
         sc = ShardedSumcheck(B.Sumcheck.from_shard(n, d, t, rank, world), device_exchange=device_exchange)
         assert sc.device_exchange == device_exchange
+        pstream = torch.cuda.ExternalStream(sc.prover.stream_handle(), device=dev)
+        junk = torch.ones(1 << 20, device=dev)
+
+        def churn(r):
+            if busy_stream:
+                with torch.cuda.stream(pstream):
+                    junk.mul_(1.5).add_(-0.5)  # unrelated work on the prover's stream
+                if r % 2:
+                    pstream.synchronize()
         sums, pts = [], []
         for r in range(n + 1):
+            churn(r)
             s, p = sc.this_round_messages()
             sums.append(s)
             pts.append(p)
+            churn(r + 1)
             if r < n:
                 sc.move_to_next_round(ch[r])
         assert sc.replicated
@@ -126,8 +140,9 @@ def _gpu_worker(rank, world, port, n, d, seed, out_q, device_exchange=False):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,d,device_exchange", [(14, 3, False), (12, 2, False), (14, 3, True), (13, 4, True)])
-def test_sharded_hip_prover_world2_gloo(n, d, device_exchange, dev):
+@pytest.mark.parametrize("n,d,device_exchange,busy", [(14, 3, False, False), (12, 2, False, False), (14, 3, True, False),
+                                                      (13, 4, True, False), (14, 3, True, True), (12, 3, False, True)])
+def test_sharded_hip_prover_world2_gloo(n, d, device_exchange, busy, dev):
     """World-2 gloo run of the HIP shard prover: the all-gathered + XOR-ed transcript equals the
     oracle's unsharded transcript, every rank sees the same messages, and each rank's slice of the
     batched NTT matches the oracle. device_exchange=True runs the RCCL path's protocol (message
@@ -136,7 +151,7 @@ def test_sharded_hip_prover_world2_gloo(n, d, device_exchange, dev):
     seed = 700 + n + d
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    mp.spawn(_gpu_worker, args=(2, _free_port(), n, d, seed, q, device_exchange), nprocs=2, join=True)
+    mp.spawn(_gpu_worker, args=(2, _free_port(), n, d, seed, q, device_exchange, busy), nprocs=2, join=True)
     got = dict()
     for _ in range(2):
         rank, s, p, ok = q.get(timeout=60)

@@ -311,3 +311,54 @@ def test_prover_from_asynchronous_ntt_output(dev):
     assert np.array_equal(got_p, want_p)
     exp = O.antt128(_rand(4 * (1 << n) * d, 4242).reshape(d, 1 << n, 4)[1], n, 0)
     assert np.array_equal(host.reshape(d, 1 << n, 4)[1], exp)
+
+
+@pytest.mark.parametrize("n,d,pattern", [(12, 3, "busy"), (11, 2, "slow"), (13, 4, "busy+slow")])
+def test_round_server_with_other_work_and_slow_host(n, d, pattern, dev):
+    """The last rounds (<= 512 evaluations per column) run on the resident round server
+    (sumcheck.hip sc_server). Unrelated kernels queued on the prover's own stream while the server
+    waits for a challenge ("busy", the host then waits for them), and a host slower than the server's
+    bounded wait ("slow": the server ends and is relaunched for the next challenge) must neither
+    deadlock nor change the transcript, which is checked word for word against the oracle."""
+    import time
+
+    import torch
+    ev, ch = _case(n, d, 6060 + n + d)
+    bs = O.bitslice128(ev)
+    want_s, want_p = O.sumcheck_run(bs, n, d, 1, ch)
+    sc = B.Sumcheck(n, d, True, bs)
+    ps = torch.cuda.ExternalStream(sc.stream_handle(), device=dev)
+    junk = torch.ones(1 << 20, device=dev)
+    for r in range(n + 1):
+        s, p = sc.this_round_messages()
+        assert np.array_equal(s, want_s[r]), "round %d sum" % r
+        assert np.array_equal(p, want_p[r]), "round %d points" % r
+        if "busy" in pattern:
+            with torch.cuda.stream(ps):
+                junk.mul_(1.5).add_(-0.5)
+            ps.synchronize()
+        if "slow" in pattern and r % 2:
+            time.sleep(0.002)  # 2 ms: ten times the server's wait
+        if r < n:
+            sc.move_to_next_round(ch[r])
+    sc.close()
+
+
+def test_round_server_abandoned_prover(dev):
+    """A prover destroyed while its round server waits for the next challenge releases it: the
+    stream drains and a new prover on the same device runs a correct transcript afterwards."""
+    import torch
+    n, d = 10, 3
+    ev, ch = _case(n, d, 7070)
+    bs = O.bitslice128(ev)
+    sc = B.Sumcheck(n, d, True, bs)
+    for r in range(n - 2):  # deep enough that the server is running
+        sc.this_round_messages()
+        sc.move_to_next_round(ch[r])
+    sc.close()
+    torch.cuda.synchronize()
+    want_s, want_p = O.sumcheck_run(bs, n, d, 1, ch)
+    sc = B.Sumcheck(n, d, True, bs)
+    got_s, got_p = _transcript(sc, n, ch)
+    sc.close()
+    assert np.array_equal(got_s, want_s) and np.array_equal(got_p, want_p)
