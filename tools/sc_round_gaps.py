@@ -15,10 +15,11 @@ def main():
                 continue
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
     rows.sort()
-    # one protocol run = nvars folds + nvars + 1 messages launches (+ sc_post for big grids);
-    # walk back from the end to the (nvars + 1)-th messages launch counted from the end
-    msgs = [i for i, r in enumerate(rows) if "sc_messages" in r[2]]
-    first = msgs[-(nvars + 1)]
+    # a protocol run starts with round 0's messages launch, the only messages launch not preceded
+    # by a fold (the last rounds may run inside one sc_server launch): take the last such start
+    starts = [i for i, r in enumerate(rows)
+              if "sc_messages" in r[2] and (i == 0 or "sc_fold" not in rows[i - 1][2])]
+    first = starts[-1]
     run = rows[first:]
     t0 = run[0][0]
     busy = sum(e - s for s, e, _ in run)
@@ -32,7 +33,7 @@ def main():
         gap = (s - prev_end) / 1e3 if prev_end is not None else 0.0
         line.append("%s %.1f (+%.1f)" % (short, (e - s) / 1e3, gap))
         prev_end = e
-        if "sc_fold" in name:
+        if "sc_fold" in name or "sc_server" in name:
             print("round %2d: %s" % (rnd, "  ".join(line)))
             line = []
             rnd += 1
