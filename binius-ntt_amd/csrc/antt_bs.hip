@@ -110,7 +110,7 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcn
 // issued into registers right after the current tile reaches LDS, so they are in flight during
 // the stages instead of exposed at the start of the next tile.
 template <int L, int ROLE, int FMAX, bool PF>
-__global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
+__device__ __forceinline__ void bs_pass_body(const BsParams& P, size_t tile0) {
 	extern __shared__ uint32_t lds[];
 	constexpr int NT = 64 * L;
 	constexpr bool IN_COMPACT = ROLE == ROLE_FIRST || ROLE == ROLE_SINGLE;
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 		if (TR) tr[7] += ts() - t_a;
 	};
 
-	size_t tile = blockIdx.x;
+	size_t tile = tile0;
 	geo(tile, outer, outer_off, coset, dst, src);
 	if (PF) issue(src, outer_off);
 	for (;;) {
@@ -426,6 +426,13 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 		for (int i = 0; i < 8; i++) o[i] = tr[i];
 	}
 }
+
+template <int L, int ROLE, int FMAX, bool PF>
+__global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
+	bs_pass_body<L, ROLE, FMAX, PF>(P, blockIdx.x);
+}
+
+
 
 // ------------------------------------------------------------------------------------
 // Lane-split passes (small launches). A pass of T tiles runs 4T waves above; below two tiles per CU
@@ -989,6 +996,7 @@ const void* bs_pass_kernel(bn_antt_plan* plan, int i) {
 	const bool pf = kn.persist && (kn.pf_mode == 2 || (kn.pf_mode == 1 && fmax <= 8));
 	return kernel_for(plan->limbs, pass.role, fmax, pf);
 }
+
 
 int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st) {
 	size_t n_passes = 0;
