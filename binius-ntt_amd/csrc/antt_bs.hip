@@ -432,6 +432,42 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 	bs_pass_body<L, ROLE, FMAX, PF>(P, blockIdx.x);
 }
 
+#ifdef BN_DEV
+// ------------------------------------------------------------------------------------
+// Experiment (development build only, BN_PERSIST3=1, tools/c3_persist_ab.sh): a
+// three-pass plan whose passes have at most two tiles per CU (one 2^20 transform: 256 tiles each)
+// as ONE launch of the variant-1 pass bodies with a grid-wide barrier between the passes instead of
+// kernel boundaries. Every work-group is resident, so the barrier cannot deadlock. Measured 0.157
+// ms against 0.0825 ms for the three launches: not used.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned target) {
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		__threadfence();  // agent-scope release of this work-group's stores (other XCDs read them)
+		atomicAdd(bar, 1u);
+		while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(1);
+	}
+	__syncthreads();
+}
+
+struct BsParams3 {
+	BsParams p[3];
+};
+template <int F0, int F1>
+__global__ __launch_bounds__(256, 2) void antt_bs_persist3(BsParams3 Q, unsigned* bar, unsigned base) {
+	bs_pass_body<4, ROLE_FIRST, F0, false>(Q.p[0], blockIdx.x);
+	grid_barrier(bar, base + gridDim.x);
+	bs_pass_body<4, ROLE_MID, F1, false>(Q.p[1], blockIdx.x);
+	grid_barrier(bar, base + 2 * gridDim.x);
+	bs_pass_body<4, ROLE_LAST, 32, false>(Q.p[2], blockIdx.x);
+}
+
+static const void* persist3_kernel(int f0, int f1) {
+	if (f0 <= 8) return f1 <= 8 ? (const void*)antt_bs_persist3<8, 8> : (const void*)antt_bs_persist3<8, 32>;
+	return f1 <= 8 ? (const void*)antt_bs_persist3<32, 8> : (const void*)antt_bs_persist3<32, 32>;
+}
+#endif
+
 
 
 // ------------------------------------------------------------------------------------
@@ -849,6 +885,11 @@ int bs_prepare(bn_antt_plan* plan) {
 					                           (int)lds_bytes(L)));
 	for (int role = 0; role < 4; role++)
 		BN_HIP(hipFuncSetAttribute(split_kernel_for(role), hipFuncAttributeMaxDynamicSharedMemorySize, (int)split_lds_bytes()));
+#ifdef BN_DEV
+	for (int f0 : {8, 32})
+		for (int f1 : {8, 32})
+			BN_HIP(hipFuncSetAttribute(persist3_kernel(f0, f1), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(4)));
+#endif
 	int rc = rr_prepare(plan);
 	if (rc != BN_OK) return rc;
 	int cus = 0;
@@ -998,10 +1039,49 @@ const void* bs_pass_kernel(bn_antt_plan* plan, int i) {
 }
 
 
+#ifdef BN_DEV
+static int launch_persist3(bn_antt_plan* plan, const BsPass* passes, const uint32_t* d_in, uint32_t* d_out, size_t batch,
+                           hipStream_t st) {
+	static unsigned* d_bar = nullptr;
+	static unsigned gen = 0;
+	if (!d_bar) {
+		BN_HIP(hipMalloc(&d_bar, sizeof(unsigned)));
+		BN_HIP(hipMemset(d_bar, 0, sizeof(unsigned)));
+	}
+	BsParams3 q;
+	memset(&q, 0, sizeof q);
+	size_t ntiles = 0;
+	for (int i = 0; i < 3; i++) {
+		q.p[i].src = d_in;
+		q.p[i].dst = d_out;
+		q.p[i].log_h = plan->log_h;
+		q.p[i].log_rate = plan->log_rate;
+		q.p[i].p = passes[i];
+		ntiles = (batch << plan->log_rate) << passes[i].n_outer;
+		q.p[i].ntiles = ntiles;
+	}
+	unsigned base = gen * 2u * (unsigned)ntiles;
+	gen++;
+	int rc = timing_begin(plan, 0, st);
+	if (rc != BN_OK) return rc;
+	void* args[] = {&q, &d_bar, &base};
+	BN_HIP(hipLaunchKernel(persist3_kernel(pass_fmax(passes[0]), pass_fmax(passes[1])), dim3((unsigned)ntiles), dim3(256), args,
+	                       lds_bytes(4), st));
+	return timing_end(plan, 0, st);
+}
+#endif
+
 int launch_bs(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st) {
 	size_t n_passes = 0;
 	const BsPass* passes = bs_passes(plan, &n_passes);
 	const BsDevKnobs kn = dev_knobs();
+#ifdef BN_DEV
+	if (getenv("BN_PERSIST3") && n_passes == 3 && plan->limbs == 4) {
+		bool ok = true;
+		for (int i = 0; i < 3; i++) ok = ok && ((batch << plan->log_rate) << passes[i].n_outer) <= (size_t)2 * (size_t)plan->num_cus;
+		if (ok) return launch_persist3(plan, passes, d_in, d_out, batch, st);
+	}
+#endif
 	const size_t npass = std::min(n_passes, kn.max_passes);
 	for (size_t i = 0; i < npass; i++) {
 		int rc = launch_one(plan, passes[i], (int)i, d_in, d_out, batch, st, kn);
