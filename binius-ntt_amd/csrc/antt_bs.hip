@@ -911,7 +911,7 @@ const BsPass* bs_passes(bn_antt_plan* plan, size_t* n_passes) {
 }
 
 struct BsDevKnobs {
-	int pf_mode = 0, dbg = 0, stop_stage = -1, split = -1;
+	int pf_mode = 0, dbg = 0, stop_stage = -1, split = -1, mid_pf = -1;
 	bool persist = true, trace = false;
 	size_t max_passes = ~(size_t)0;
 };
@@ -929,6 +929,7 @@ static BsDevKnobs dev_knobs() {
 	if (const char* e = getenv("BN_DEBUG_FLAGS")) k.dbg = atoi(e);
 	if (const char* e = getenv("BN_DEBUG_STOP_STAGE")) k.stop_stage = atoi(e);
 	if (const char* e = getenv("BN_SPLIT")) k.split = atoi(e);  // 0: never lane-split, 1: always
+	if (const char* e = getenv("BN_MID_PF")) k.mid_pf = atoi(e);  // 1: middle passes on antt_rr_mid_pf
 	k.trace = getenv("BN_TRACE") != nullptr;
 #endif
 	return k;
@@ -938,6 +939,22 @@ static BsDevKnobs dev_knobs() {
 // lane-split (antt_bs3_pass: two waves per product, two waves per SIMD instead of one). 2^20 A/B
 // (tools/ab_split.sh): upper GF(2^32) pass 0.0139 vs 0.0158 ms, bottom pass 0.0514 vs 0.0496 ms,
 // so the bottom pass keeps one wave per limb
+// Development build only (BN_MID_PF=1): GF(2^16/32) middle passes on antt_rr_mid_pf, the
+// register-tile kernel that hides the next tile's loads. Measured slower than antt_bs_pass at 2^24
+// (pass 1 0.224-0.229 vs 0.189-0.193 ms), so the product never selects it.
+static bool use_mid_pf(const bn_antt_plan* plan, const BsPass& pass, size_t ntiles, const BsDevKnobs& kn) {
+#ifdef BN_DEV
+	if (kn.mid_pf != 1) return false;
+	if (plan->variant != 5 || plan->limbs != 4 || pass.role != ROLE_MID || pass_fmax(pass) <= 8) return false;
+	RtPass rt;
+	if (make_rt(pass, false, &rt) != BN_OK) return false;
+	return ntiles >= (size_t)8 * (size_t)plan->num_cus;
+#else
+	(void)plan, (void)pass, (void)ntiles, (void)kn;
+	return false;
+#endif
+}
+
 static bool use_split(const bn_antt_plan* plan, const BsPass& pass, size_t ntiles, const BsDevKnobs& kn) {
 	if (plan->limbs != 4 || pass_fmax(pass) <= 8) return false;
 	if (kn.split >= 0) return kn.split != 0;
@@ -960,6 +977,9 @@ static int launch_one(bn_antt_plan* plan, const BsPass& pass, int i, const uint3
 	prm.p = pass;
 	prm.p.stop_j = kn.stop_stage < 0 ? 0 : std::max(0, std::min(prm.p.k, kn.stop_stage - prm.p.lo));
 	const size_t ntiles = (batch << plan->log_rate) << pass.n_outer;
+#ifdef BN_DEV
+	if (use_mid_pf(plan, pass, ntiles, kn)) return rr_launch_mid_pf(plan, i, d_in, d_out, batch, st);
+#endif
 	if (use_split(plan, pass, ntiles, kn)) {
 		prm.ntiles = ntiles;
 		prm.trace = nullptr;
@@ -1033,6 +1053,9 @@ const void* bs_pass_kernel(bn_antt_plan* plan, int i) {
 	// the kernel for ONE transform (bench / profiles): a batched launch of the same pass may pick
 	// another (the lane-split and prefetching kernels depend on the tile count)
 	const size_t ntiles = ((size_t)1 << plan->log_rate) << pass.n_outer;
+#ifdef BN_DEV
+	if (use_mid_pf(plan, pass, ntiles, kn)) return rr_mid_pf_kernel(pass);
+#endif
 	if (use_split(plan, pass, ntiles, kn)) return split_kernel_for(pass.role);
 	const bool pf = kn.persist && (kn.pf_mode == 2 || (kn.pf_mode == 1 && fmax <= 8));
 	return kernel_for(plan->limbs, pass.role, fmax, pf);

@@ -62,5 +62,8 @@ int rr_prepare(bn_antt_plan* plan);
 int rr_launch_pass(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st);
 const void* rr_pass_kernel(bn_antt_plan* plan, const BsPass& pass);
 const void* bs_pass_kernel(bn_antt_plan* plan, int i);
+// middle passes with the next tile prefetched by LDS-DMA (antt_rr.hip antt_rr_mid_pf)
+int rr_launch_mid_pf(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st);
+const void* rr_mid_pf_kernel(const BsPass& pass);
 
 }  // namespace bn

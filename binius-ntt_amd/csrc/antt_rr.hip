@@ -44,6 +44,7 @@ struct RrParams {
 	const uint32_t* src;
 	uint32_t* dst;
 	int log_h, log_rate;
+	size_t ntiles;  // antt_rr_mid_pf (persistent grid): tiles of the pass
 	RtPass p;
 };
 
@@ -318,6 +319,194 @@ __global__ __launch_bounds__(64 * L, RrOcc<ROLE>::value) void antt_rr_pass(RrPar
 	}
 }
 
+// ------------------------------------------------------------------------------------
+// Middle passes with the next tile's loads hidden (persistent grid, two work-groups per CU). The
+// LDS-tile kernel (antt_bs_pass) has no room to overlap a tile's loads with its stages: the tile
+// fills the LDS (74 KB, two per CU) and the circuits the VGPRs, so each tile's loads are exposed
+// (the dev build's no-load run of pass 1 at 2^24 is 17 % faster). Here the tile lives in VGPRs (as
+// antt_rr_pass) and the LDS holds, per wave,
+//   * 16 KB: the NEXT tile's limb plane, requested by LDS-DMA (global_load_lds, no VGPRs) as soon as
+//     this tile's plane has been read out of the same region, landing while this tile computes;
+//   * 4 KB: output staging, 32 blocks at a time (coalesced 1 KiB stores of whole lines).
+// 4 x 20 KB = 80 KB per work-group, two per CU. Same tiles, tables and HBM layout as antt_rr_pass.
+// Development build only (BN_MID_PF=1): parity green (GF(2^128) suite + MD5 tables), but pass 1 at
+// 2^24 measured 0.224-0.229 ms against 0.189-0.193 ms for antt_bs_pass (three A/B pairs, round 5):
+// the register tile's exchanges cost more than the hidden loads give back.
+// ------------------------------------------------------------------------------------
+#ifdef BN_DEV
+__device__ __forceinline__ int opaque_lane() {
+	int x = (int)threadIdx.x & 63;
+	asm volatile("" : "=v"(x) : "0"(x));
+	return x;
+}
+constexpr int kPreWords = 128 * 32;  // per wave: a whole limb plane, chunk-swizzled (no padding)
+constexpr int kOutWords = 32 * 32;   // per wave: 32 blocks of output staging, chunk-swizzled
+
+template <int FMAX>
+__global__ __launch_bounds__(256, 2) void antt_rr_mid_pf(RrParams P) {
+	extern __shared__ uint32_t lds[];
+	constexpr int L = 4;
+	const RtPass& ps = P.p;
+	const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+	// the lane index is re-read opaquely at every tile: lane-derived addresses hoisted out of the tile
+	// loop would stay live through the circuits and spill
+	int lane = threadIdx.x & 63;
+	const size_t n = (size_t)1 << P.log_h;
+	char* pre = (char*)(lds + w * kPreWords);
+	uint32_t* ost = lds + L * kPreWords + w * kOutWords;
+	auto tile_off = [&](int q) -> size_t {
+		size_t off = 0;
+#pragma unroll
+		for (int m = 0; m < kBlkBits; m++) off |= (size_t)((q >> m) & 1) << ps.bb[m];
+		return off;
+	};
+	struct Geo {
+		size_t outer, ooff;
+		int coset;
+		uint32_t* d;
+	};
+	auto geo = [&](size_t t) -> Geo {
+		Geo g;
+		g.outer = t & (((size_t)1 << ps.n_outer) - 1);
+		const size_t rest = t >> ps.n_outer;
+		g.coset = (int)(rest & ((1u << P.log_rate) - 1));
+		const size_t batch = rest >> P.log_rate;
+		g.ooff = 0;
+		for (int m = 0; m < ps.n_outer; m++) g.ooff |= ((g.outer >> m) & 1) << ps.ob[m];
+		g.d = P.dst + (((batch << P.log_rate) + (size_t)g.coset) * n) * L;
+		return g;
+	};
+	// the tile's limb plane w by LDS-DMA into `pre`: instruction 8 h + r fetches slots 8 r .. 8 r + 7 of
+	// half h (blocks + 64 h), lane L chunk (L & 7) ^ f(slot) of slot 8 r + L / 8 (antt_rr_pass's layout)
+	auto dma = [&](const Geo& g) {
+#pragma unroll
+		for (int h = 0; h < 2; h++)
+#pragma unroll
+			for (int r = 0; r < 8; r++) {
+				const int sl = 8 * r + (lane >> 3), c = (lane & 7) ^ ((sl >> 1) & 7);
+				__builtin_amdgcn_global_load_lds((const void*)(g.d + (g.ooff | tile_off(sl + 64 * h)) * L + 32 * w + 4 * c),
+				                                 (__attribute__((address_space(3))) void*)(pre + 8192 * h + 1024 * r), 16, 0, 0);
+			}
+	};
+	size_t tile = blockIdx.x;
+	Geo cur = geo(tile);
+	dma(cur);
+	const int mlow = ps.mlow;
+	for (;;) {
+		lane = opaque_lane();
+		const int G = coords(lane);
+		// work-group-uniform twiddle part (outer and coset bits) of stage j, held by lane j
+		uint32_t cuv = 0;
+		if (lane < ps.k) {
+			for (int m = 0; m < ps.n_outer; m++)
+				if ((cur.outer >> m) & 1) cuv ^= ps.two[lane][m];
+			for (int b = 0; b < P.log_rate; b++)
+				if ((cur.coset >> b) & 1) cuv ^= ps.twc[lane][b];
+		}
+		auto ucu = [&](int j) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)cuv, j); };
+		// ---- this tile's plane: its DMA is done once all but the previous tile's 16 stores are
+		uint32_t R0[32], R1[32];
+#ifdef BN_MID_PF_ASM
+		{
+			// read in inline asm: the compiler cannot tell this tile's DMA from the previous tile's
+			// stores and would wait for both (vmcnt(0)) before an LDS read it can see
+			typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+			v4u x[16];
+			const uint32_t a0 = (uint32_t)(uintptr_t)(pre + 128 * G);
+			const uint32_t sw = 16u * (uint32_t)((G >> 1) & 7);
+			uint32_t ad[8];
+#pragma unroll
+			for (int c = 0; c < 8; c++) ad[c] = a0 + ((16u * c) ^ sw);
+			asm volatile(
+			    "s_waitcnt vmcnt(16)\n"
+			    "ds_read_b128 %0, %16\n ds_read_b128 %1, %17\n ds_read_b128 %2, %18\n ds_read_b128 %3, %19\n"
+			    "ds_read_b128 %4, %20\n ds_read_b128 %5, %21\n ds_read_b128 %6, %22\n ds_read_b128 %7, %23\n"
+			    "ds_read_b128 %8, %16 offset:8192\n ds_read_b128 %9, %17 offset:8192\n ds_read_b128 %10, %18 offset:8192\n"
+			    "ds_read_b128 %11, %19 offset:8192\n ds_read_b128 %12, %20 offset:8192\n ds_read_b128 %13, %21 offset:8192\n"
+			    "ds_read_b128 %14, %22 offset:8192\n ds_read_b128 %15, %23 offset:8192\n"
+			    "s_waitcnt lgkmcnt(0)"
+			    : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3]), "=&v"(x[4]), "=&v"(x[5]), "=&v"(x[6]), "=&v"(x[7]),
+			      "=&v"(x[8]), "=&v"(x[9]), "=&v"(x[10]), "=&v"(x[11]), "=&v"(x[12]), "=&v"(x[13]), "=&v"(x[14]), "=&v"(x[15])
+			    : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), "v"(ad[5]), "v"(ad[6]), "v"(ad[7])
+			    : "memory");
+#pragma unroll
+			for (int c = 0; c < 8; c++) {
+				R0[4 * c] = x[c].x, R0[4 * c + 1] = x[c].y, R0[4 * c + 2] = x[c].z, R0[4 * c + 3] = x[c].w;
+				R1[4 * c] = x[8 + c].x, R1[4 * c + 1] = x[8 + c].y, R1[4 * c + 2] = x[8 + c].z, R1[4 * c + 3] = x[8 + c].w;
+			}
+		}
+#else
+		asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			uint32_t* R = h ? R1 : R0;
+#pragma unroll
+			for (int c = 0; c < 8; c++) {
+				const uint4 v = *(const uint4*)(pre + 8192 * h + 128 * G + 16 * (c ^ ((G >> 1) & 7)));
+				R[4 * c] = v.x, R[4 * c + 1] = v.y, R[4 * c + 2] = v.z, R[4 * c + 3] = v.w;
+			}
+		}
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read out: the region takes the next tile
+#endif
+		const size_t next = tile + gridDim.x;
+		const bool has_next = next < P.ntiles;
+		Geo nxt = cur;
+		if (has_next) {
+			nxt = geo(next);
+			dma(nxt);
+		}
+
+		// ---- block stages on tile bits 6 .. mlow (antt_rr_pass)
+#pragma unroll 1
+		for (int m = kBlkBits - 1; m >= mlow; m--) {
+			if (m < kBlkBits - 1) xchg(R0, R1, lane, m);
+			uint32_t tw = ucu(ps.jm[m]);
+#pragma unroll
+			for (int b = 0; b < 6; b++) tw ^= ps.tau[m][b] & bitmask(lane, b);
+			__builtin_amdgcn_sched_barrier(0);
+			fma_tw<FMAX>(ps.field_m[m], tw, R1, R0);  // u ^= w * v
+			__builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+			for (int i = 0; i < 32; i++) R1[i] ^= R0[i];  // v ^= u
+		}
+
+		// ---- bitsliced out, 32 blocks per round through this wave's 4 KB: round (h, hh) stages the
+		// blocks of R_h held by lanes 32 hh .. 32 hh + 31 (slot G & 31, chunk-swizzled), then the wave
+		// stores them as four 1 KiB runs of whole 128-byte lines (antt_rr_pass's block mapping)
+		const int lowm = (1 << mlow) - 1;
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			const uint32_t* R = h ? R1 : R0;
+#pragma unroll
+			for (int hh = 0; hh < 2; hh++) {
+				if ((G >> 5) == hh) {
+					const int so = G & 31;
+#pragma unroll
+					for (int c = 0; c < 8; c++)
+						*(uint4*)(ost + 32 * so + 4 * (c ^ ((so >> 1) & 7))) = make_uint4(R[4 * c], R[4 * c + 1], R[4 * c + 2], R[4 * c + 3]);
+				}
+				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+				for (int r = 0; r < 4; r++) {
+					const int so = 8 * r + (lane >> 3), c = lane & 7;
+					const int sl = 32 * hh + so;
+					const int q = ((sl & ~lowm) << 1) | (h << mlow) | (sl & lowm);
+					const uint4 v = *(const uint4*)(ost + 32 * so + 4 * (c ^ ((so >> 1) & 7)));
+					const uint32_t o[4] = {v.x, v.y, v.z, v.w};
+					st4(cur.d + (cur.ooff | tile_off(q)) * L + 32 * w + 4 * c, o);
+				}
+				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read out before the next round's writes
+			}
+		}
+		if (!has_next) break;
+		tile = next;
+		cur = nxt;
+	}
+}
+
+static size_t mid_pf_lds_bytes() { return (size_t)4 * (kPreWords + kOutWords) * sizeof(uint32_t); }
+#endif  // BN_DEV
+
 template <int L, int FMAX>
 static const void* kernel_f(int role) {
 	switch (role) {
@@ -341,6 +530,10 @@ static size_t lds_bytes(int L, int role) {
 
 int rr_prepare(bn_antt_plan* plan) {
 	(void)plan;
+#ifdef BN_DEV
+	for (const void* f : {(const void*)rr::antt_rr_mid_pf<16>, (const void*)rr::antt_rr_mid_pf<32>})
+		BN_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rr::mid_pf_lds_bytes()));
+#endif
 	for (int L : {1, 4})
 		for (int role = 0; role < 4; role++)
 			for (int f : {8, 16, 32})
@@ -365,6 +558,7 @@ int rr_launch_pass(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* d_
 	prm.dst = d_out;
 	prm.log_h = plan->log_h;
 	prm.log_rate = plan->log_rate;
+	prm.ntiles = (batch << plan->log_rate) << pass.n_outer;
 	int rc = make_rt(pass, bottom, &prm.p);
 	if (rc != BN_OK) BN_FAIL(rc, "register-tile pass table: stage bits are not the top tile bits");
 	const int L = plan->limbs;
@@ -376,6 +570,38 @@ int rr_launch_pass(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* d_
 	                       rr::lds_bytes(L, pass.role), st));
 	return timing_end(plan, i, st);
 }
+
+#ifdef BN_DEV
+// a middle pass (bitsliced in and out, GF(2^16/32) twiddles) on the prefetching register-tile kernel
+int rr_launch_mid_pf(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st) {
+	size_t n_passes = 0;
+	const BsPass* passes = bs_passes(plan, &n_passes);
+	if (i < 0 || (size_t)i >= n_passes) BN_FAIL(BN_ERR_INVALID, "pass %d out of range", i);
+	const BsPass& pass = passes[i];
+	if (pass.role != ROLE_MID || plan->limbs != 4) BN_FAIL(BN_ERR_UNSUPPORTED, "prefetching kernel: middle passes of GF(2^128) plans only");
+	rr::RrParams prm;
+	prm.src = d_in;
+	prm.dst = d_out;
+	prm.log_h = plan->log_h;
+	prm.log_rate = plan->log_rate;
+	int rc = make_rt(pass, false, &prm.p);
+	if (rc != BN_OK) BN_FAIL(rc, "register-tile pass table: stage bits are not the top tile bits");
+	const size_t ntiles = (batch << plan->log_rate) << pass.n_outer;
+	prm.ntiles = ntiles;
+	const size_t grid = std::min(ntiles, (size_t)2 * (size_t)plan->num_cus);
+	rc = timing_begin(plan, i, st);
+	if (rc != BN_OK) return rc;
+	void* args[] = {&prm};
+	const void* k = pass_fmax(pass) <= 16 ? (const void*)rr::antt_rr_mid_pf<16> : (const void*)rr::antt_rr_mid_pf<32>;
+	BN_HIP(hipLaunchKernel(k, dim3((unsigned)grid), dim3(256), args, rr::mid_pf_lds_bytes(), st));
+	return timing_end(plan, i, st);
+}
+
+const void* rr_mid_pf_kernel(const BsPass& pass) {
+	return pass_fmax(pass) <= 16 ? (const void*)rr::antt_rr_mid_pf<16> : (const void*)rr::antt_rr_mid_pf<32>;
+}
+
+#endif  // BN_DEV
 
 int launch_rr(bn_antt_plan* plan, const uint32_t* d_in, uint32_t* d_out, size_t batch, hipStream_t st) {
 	size_t n_passes = 0;

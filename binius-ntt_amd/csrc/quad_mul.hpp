@@ -69,8 +69,11 @@ __device__ __forceinline__ void sst(const Slot& S, int r, const uint32_t* x) { s
 // GF(2^128) product on a quad. On entry slot row l holds limb l of the first operand and row 4+l
 // limb l of the second — or, with B_SHARED, the second operand is the unswizzled 128-word B
 // shared by every quad (the fold's broadcast challenge). On exit row l holds limb l of the product.
+// skip_mid (development-build timing experiment only): the third circuit is replaced by its
+// operand sum, i.e. 8 instead of 12 circuits per product (wrong results; an upper bound on what a
+// 9-circuit Karatsuba top level could save in the kernels that call this).
 template <bool B_SHARED>
-__device__ __forceinline__ void quad_mul(const Slot& S, const uint32_t* B, int l) {
+__device__ __forceinline__ void quad_mul(const Slot& S, const uint32_t* B, int l, bool skip_mid = false) {
 	wsync();
 	const int ia = l & 1, jb = (l == 1 || l == 2) ? 1 : 0;
 	const int ra = 2 * ia, rb = 4 + 2 * jb;  // rows of a0 (a1 = ra + 1) and b0 (b1 = rb + 1)
@@ -116,7 +119,12 @@ __device__ __forceinline__ void quad_mul(const Slot& S, const uint32_t* B, int l
 	sst(S, 2 * l, z);
 	sst(S, 2 * l + 1, y);
 	__builtin_amdgcn_sched_barrier(0);
-	bsm5_mul(sa, sb, x);  // (a0+a1)(b0+b1)
+	if (skip_mid) {
+#pragma unroll
+		for (int i = 0; i < 32; i++) x[i] = sa[i] ^ sb[i];
+	} else {
+		bsm5_mul(sa, sb, x);  // (a0+a1)(b0+b1)
+	}
 	__builtin_amdgcn_sched_barrier(0);
 	sld(y, S, 2 * l + 1);
 #pragma unroll

@@ -178,6 +178,15 @@ __device__ __forceinline__ void post_points(const ScArgs& A, int t) {
 	if (t == 0) __hip_atomic_store(A.res + kResSeq, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Timing-experiment builds only (make BUILD=build-x LIBDIR=lib-x EXTRA=-DBN_SC_SKIP_MID): the
+// big rounds' quad products run 8 of their 12 GF(2^32) circuits (wrong results), the upper bound
+// on what a 9-circuit Karatsuba top level could save.
+#ifdef BN_SC_SKIP_MID
+constexpr bool kSkipMid = true;
+#else
+constexpr bool kSkipMid = false;
+#endif
+
 // Products run on a group of G lanes: G = 4 (quad_mul, throughput) for launches that fill the
 // GPU, G = 16 (hex_mul, about a third of the latency) for the last rounds' small launches, G = 64
 // (wide_mul, GF(2^16) circuits on 36 lanes) for the smallest. Lanes l < 4 of a group hold the
@@ -189,9 +198,9 @@ struct Grp {
 	static constexpr int kSlotsWords = kGroups * kSlotWords;
 };
 template <int G, bool B_SHARED>
-__device__ __forceinline__ void grp_mul(const Slot& S, const uint32_t* B, int l) {
+__device__ __forceinline__ void grp_mul(const Slot& S, const uint32_t* B, int l, bool skip_mid = false) {
 	if constexpr (G == 4)
-		quad_mul<B_SHARED>(S, B, l);
+		quad_mul<B_SHARED>(S, B, l, skip_mid);
 	else if constexpr (G == 16)
 		hex_mul<B_SHARED>(S, B, l);
 	else
@@ -248,7 +257,7 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_messages(ScArgs A) {
 #ifdef BN_DEV
 			if (A.dbg & 2) continue;
 #endif
-			if (j > 0) grp_mul<G, false>(S, nullptr, l);
+			if (j > 0) grp_mul<G, false>(S, nullptr, l, kSkipMid);
 		}
 		wsync();
 		if (l < 4) {
@@ -339,7 +348,7 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold(ScArgs A) {
 #ifdef BN_DEV
 		if (!(A.dbg & 2))
 #endif
-		grp_mul<G, true>(S, R, l);
+		grp_mul<G, true>(S, R, l, kSkipMid);
 		if (l >= 4) return;
 		// lo is re-read (cache-resident) rather than kept live across the quad product; the hex
 		// product leaves the registers for it
@@ -384,7 +393,7 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_coal(ScArgs A) {
 #ifdef BN_DEV
 	if (!(A.dbg & 2))
 #endif
-	quad_mul<true>(S, R, l);
+	quad_mul<true>(S, R, l, kSkipMid);
 	wsync();
 #pragma unroll
 	for (int i = 0; i < 8; i++) {
