@@ -164,7 +164,7 @@ def limb0_check(d_out, log_h):
             "source": "additive_ntt_hashes[0][%d] (src/ulvt/ntt/tests/test_ntt.cu:52-124)" % log_h}
 
 
-PMC_FILE = os.path.join("profiles", "r04", "pmc_kernels.json")
+PMC_FILE = os.path.join("profiles", "r05", "pmc_kernels.json")
 
 
 def lib_sha256():
