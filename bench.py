@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--sc-log-n", type=int, default=28)
     ap.add_argument("--sc-d", type=int, default=3)
     ap.add_argument("--sc-runs", type=int, default=2)
+    ap.add_argument("--sc-exchange", choices=("auto", "host", "device"), default="auto",
+                    help="config-5 sumcheck message exchange: auto = device sink on nccl, host-staged "
+                         "on gloo; device on gloo stages the sink through host memory")
     ap.add_argument("--variant", type=int, default=None, help="NTT kernel variant (default: the plan's choice)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the launch path: the --gpus relaunch, process-group setup (gloo), "
@@ -229,7 +232,8 @@ def c5_sumcheck(a, B, D, torch, dev, local, rank, world, backend, barrier, max_o
 
     def run_sumcheck(check):
         prover = B.Sumcheck.from_shard(N, d, shard, rank, world, device=local)
-        sc = D.ShardedSumcheck(prover, group)
+        dx = None if a.sc_exchange == "auto" else a.sc_exchange == "device"
+        sc = D.ShardedSumcheck(prover, group, device_exchange=dx)
         exch.append(sc)
         barrier()
         torch.cuda.synchronize(dev)
@@ -272,7 +276,9 @@ def c5_sumcheck(a, B, D, torch, dev, local, rank, world, backend, barrier, max_o
         "per_gpu_alg_gbps": alg / world / tsc / 1e9,
         "collective": "all_gather_into_tensor (%s) + XOR" % (backend if world > 1 else "none, world 1"),
         "exchange_ms": ex_ms, "exchange_rounds": last.exchange_rounds,
-        "exchange_ms_per_round": ex_ms / last.exchange_rounds if last.exchange_rounds else None}
+        "exchange_ms_per_round": ex_ms / last.exchange_rounds if last.exchange_rounds else None,
+        "exchange_path": "device sink" if last.device_exchange else "host-staged",
+        "messages_ms_per_round": max_over_ranks(last.round_seconds * 1e3) / N}
     del shard
     return res
 
