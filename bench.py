@@ -470,9 +470,11 @@ def main():
                 "pass_ms_inloop": pass_ms_inloop,
                 "transform_frac": transform_gbps / HBM_PEAK_GBPS,
                 "limiter": limiter_of(valu, achieved / HBM_PEAK_GBPS, ctr),
-                "duration_note": "kernel_ms / pass_ms are uninstrumented hipEvent timings; the rocprofv3 "
-                                 "kernel traces committed under profiles/ run ~6-9 %% longer per launch "
-                                 "(profiler overhead), so frac recomputed from them is lower by that much",
+                "duration_note": "kernel_ms / pass_ms are uninstrumented hipEvent timings of back-to-back "
+                                 "launches; in the committed rocprofv3 traces (profiles/) the timed-loop "
+                                 "launches agree within ~2 %, while the all-launch stats averages include "
+                                 "warm-up and event-bracketed launches and run ~6-9 % longer, so frac "
+                                 "recomputed from those is lower by that much",
             },
             "valu": valu,
         }

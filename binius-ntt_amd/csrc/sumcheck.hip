@@ -404,9 +404,9 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_coal(ScArgs A) {
 
 // ---------------------------------------------------------------------------------------
 // Round server for the last rounds (at most kServerMaxCur evaluations per column left): ONE
-// resident 512-thread workgroup runs every remaining round by itself. It waits for the host's
-// challenge in host-mapped control words, folds, computes the next round's messages on 16-lane
-// products and posts them exactly as sc_messages does (points, then the sequence word). A small
+// resident 768-thread workgroup runs every remaining round by itself. It waits for the host's
+// challenge in host-mapped control words, folds, computes the next round's messages on 64-lane
+// products (wide_mul) and posts them exactly as sc_messages does (points, then the sequence word). A small
 // round then costs no kernel launch, no dispatch ramp and no cross-workgroup reduction: with one
 // fold and one messages launch per round the last rounds of c4 took ~10 us (fold) + ~18 us
 // (messages) of kernel time plus ~12 us of host launches each (round-4 trace).
