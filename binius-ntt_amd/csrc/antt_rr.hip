@@ -46,7 +46,16 @@ struct RrParams {
 	int log_h, log_rate;
 	size_t ntiles;  // antt_rr_mid_pf (persistent grid): tiles of the pass
 	RtPass p;
+#ifdef BN_DEV
+	int dbg;  // BN_DEBUG_FLAGS bit 0 = no tile loads, bit 1 = no tile stores (wrong results; timing
+	          // experiments on antt_rr_pass)
+#endif
 };
+#ifdef BN_DEV
+#define RR_DBG(P) ((P).dbg)
+#else
+#define RR_DBG(P) 0
+#endif
 
 constexpr int kSlot = 36;                 // LDS words per staged block (32 + 4 pad: conflict-free b128 writes)
 constexpr int kStagePlane = 64 * kSlot;   // one limb plane of a half tile
@@ -152,17 +161,28 @@ __global__ __launch_bounds__(64 * L, RrOcc<ROLE>::value) void antt_rr_pass(RrPar
 	// block G + 64 h.
 	if (IN_COMPACT && L == 4) {
 		// compact 16-byte elements, half a tile (64 blocks) at a time through LDS: coalesced loads,
-		// limb l of block slot s at plane l, word s * kSlot + element
+		// limb l of block slot s at plane l, word s * kSlot + element. Both halves' loads are issued
+		// up front (64 VGPRs, below the stages' peak), so the second half's latency hides behind the
+		// first half's LDS round trip and transposes.
+		uint32_t gv[2][8][4];
+#pragma unroll
+		for (int h = 0; h < 2; h++)
+#pragma unroll
+			for (int r = 0; r < 8; r++) {
+				const int idx = tid + NT * r, s = idx >> 5, e = idx & 31;
+				if (RR_DBG(P) & 1)
+					gv[h][r][0] = idx, gv[h][r][1] = s, gv[h][r][2] = e, gv[h][r][3] = tid;
+				else
+					ld4(src + (ooff | tile_off(s + 64 * h) | (size_t)e) * 4, gv[h][r]);
+			}
 #pragma unroll
 		for (int h = 0; h < 2; h++) {
 			if (h) __syncthreads();  // every wave has read the first half
 #pragma unroll
 			for (int r = 0; r < 8; r++) {
 				const int idx = tid + NT * r, s = idx >> 5, e = idx & 31;
-				uint32_t v[4];
-				ld4(src + (ooff | tile_off(s + 64 * h) | (size_t)e) * 4, v);
 #pragma unroll
-				for (int l = 0; l < 4; l++) lds[l * kStagePlane + s * kSlot + e] = v[l];
+				for (int l = 0; l < 4; l++) lds[l * kStagePlane + s * kSlot + e] = gv[h][r][l];
 			}
 			__syncthreads();
 			uint32_t* R = h ? R1 : R0;
@@ -187,6 +207,7 @@ __global__ __launch_bounds__(64 * L, RrOcc<ROLE>::value) void antt_rr_pass(RrPar
 #pragma unroll
 			for (int r = 0; r < 8; r++) {
 				const int sl = 8 * r + (lane >> 3), c = (lane & 7) ^ ((sl >> 1) & 7);
+				if (RR_DBG(P) & 1) continue;
 				__builtin_amdgcn_global_load_lds((const void*)(src + (ooff | tile_off(sl + 64 * h)) * L + 32 * w + 4 * c),
 				                                 (__attribute__((address_space(3))) void*)(wr + 1024 * r), 16, 0, 0);
 			}
@@ -286,7 +307,7 @@ __global__ __launch_bounds__(64 * L, RrOcc<ROLE>::value) void antt_rr_pass(RrPar
 					uint32_t v[4];
 #pragma unroll
 					for (int l = 0; l < 4; l++) v[l] = lds[l * kStagePlane + s * kSlot + e];
-					st4(dst + (ooff | tile_off(2 * s + h) | (size_t)e) * 4, v);
+					if (!(RR_DBG(P) & 2)) st4(dst + (ooff | tile_off(2 * s + h) | (size_t)e) * 4, v);
 				}
 			}
 		} else {
@@ -313,7 +334,7 @@ __global__ __launch_bounds__(64 * L, RrOcc<ROLE>::value) void antt_rr_pass(RrPar
 				const int q = ((sl & ~lowm) << 1) | (h << mlow) | (sl & lowm);
 				const uint4 v = *(const uint4*)(wp + sl * kSlot + 4 * c);
 				const uint32_t o[4] = {v.x, v.y, v.z, v.w};
-				st4(dst + (ooff | tile_off(q)) * L + 32 * w + 4 * c, o);
+				if (!(RR_DBG(P) & 2)) st4(dst + (ooff | tile_off(q)) * L + 32 * w + 4 * c, o);
 			}
 		}
 	}
@@ -559,6 +580,10 @@ int rr_launch_pass(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* d_
 	prm.log_h = plan->log_h;
 	prm.log_rate = plan->log_rate;
 	prm.ntiles = (batch << plan->log_rate) << pass.n_outer;
+#ifdef BN_DEV
+	prm.dbg = 0;
+	if (const char* e = getenv("BN_DEBUG_FLAGS")) prm.dbg = atoi(e) & 3;
+#endif
 	int rc = make_rt(pass, bottom, &prm.p);
 	if (rc != BN_OK) BN_FAIL(rc, "register-tile pass table: stage bits are not the top tile bits");
 	const int L = plan->limbs;
@@ -588,6 +613,7 @@ int rr_launch_mid_pf(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* 
 	if (rc != BN_OK) BN_FAIL(rc, "register-tile pass table: stage bits are not the top tile bits");
 	const size_t ntiles = (batch << plan->log_rate) << pass.n_outer;
 	prm.ntiles = ntiles;
+	prm.dbg = 0;  // (development build only: this launcher exists only there)
 	const size_t grid = std::min(ntiles, (size_t)2 * (size_t)plan->num_cus);
 	rc = timing_begin(plan, i, st);
 	if (rc != BN_OK) return rc;
