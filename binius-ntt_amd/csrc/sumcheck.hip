@@ -521,7 +521,7 @@ __global__ __launch_bounds__(kSrvThreads, 1) void sc_server(SrvArgs P) {
 	const Slot S{lds + qw * Grp<kSrvG>::kSlotWords};
 	uint32_t* R = lds + kSrvGroups * Grp<kSrvG>::kSlotWords;  // the challenge, broadcast-bitsliced
 	uint32_t* accL = R + 128;                    // (kMaxD + 1) x 4 point words
-	uint32_t* ctlL = accL + 4 * (kMaxD + 1);     // [0] wake-up reason, [1] skip-p(1) flag
+	uint32_t* ctlL = accL + 4 * (kMaxD + 1);     // [0] wake-up reason, [1] skip-p(1) flag, [2..5] challenge
 	ScArgs a{};
 	a.cols = P.cols;
 	a.col_stride = P.col_stride;
@@ -541,7 +541,10 @@ __global__ __launch_bounds__(kSrvThreads, 1) void sc_server(SrvArgs P) {
 				__builtin_amdgcn_s_sleep(2);
 			}
 			ctlL[0] = why;
+			// the words the ticket publishes, read by the thread whose acquire saw it
 			ctlL[1] = __hip_atomic_load(P.ctl + kCtlSkip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			for (int i = 0; i < 4; i++)
+				ctlL[2 + i] = __hip_atomic_load(P.ctl + kCtlR + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 		}
 		__syncthreads();
 #ifdef BN_DEV
@@ -554,10 +557,7 @@ __global__ __launch_bounds__(kSrvThreads, 1) void sc_server(SrvArgs P) {
 				__hip_atomic_store(P.ctl_exit, ticket - 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 			return;
 		}
-		if (threadIdx.x < 128) {
-			const uint32_t rw = __hip_atomic_load(P.ctl + kCtlR + threadIdx.x / 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-			R[threadIdx.x] = 0u - ((rw >> (threadIdx.x % 32)) & 1u);
-		}
+		if (threadIdx.x < 128) R[threadIdx.x] = 0u - ((ctlL[2 + threadIdx.x / 32] >> (threadIdx.x % 32)) & 1u);
 		if (threadIdx.x < 4 * (kMaxD + 1)) accL[threadIdx.x] = 0;
 		__syncthreads();
 		// ---- fold: cur -> cur / 2
@@ -604,7 +604,7 @@ __global__ __launch_bounds__(kSrvThreads, 1) void sc_server(SrvArgs P) {
 	}
 }
 
-size_t srv_lds_bytes() { return ((size_t)kSrvGroups * Grp<kSrvG>::kSlotWords + 128 + 4 * (kMaxD + 1) + 2) * sizeof(uint32_t); }
+size_t srv_lds_bytes() { return ((size_t)kSrvGroups * Grp<kSrvG>::kSlotWords + 128 + 4 * (kMaxD + 1) + 6) * sizeof(uint32_t); }
 
 // quad slots + the fold's broadcast challenge (128 words) + the messages' accumulators, flag and
 // last-workgroup reduction

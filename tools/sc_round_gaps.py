@@ -2,6 +2,7 @@
 (tools/sc_trace.sh): kernel durations and the idle gaps between them, in microseconds.
   python tools/sc_round_gaps.py <run_kernel_trace.csv> <nvars>"""
 import csv
+import re
 import sys
 
 
@@ -29,7 +30,8 @@ def main():
     rnd = 0
     line = []
     for s, e, name in run:
-        short = name.split("(")[0].split("::")[-1]
+        m = re.search(r"sc_\w+(<[^>]*>)?", name)
+        short = m.group(0) if m else name[:24]
         gap = (s - prev_end) / 1e3 if prev_end is not None else 0.0
         line.append("%s %.1f (+%.1f)" % (short, (e - s) / 1e3, gap))
         prev_end = e
