@@ -362,3 +362,65 @@ def test_round_server_abandoned_prover(dev):
     got_s, got_p = _transcript(sc, n, ch)
     sc.close()
     assert np.array_equal(got_s, want_s) and np.array_equal(got_p, want_p)
+
+
+@pytest.mark.parametrize("n,d,pattern", [(15, 3, "plain"), (14, 2, "slow"), (15, 4, "busy"), (14, 3, "skip"),
+                                         (14, 3, "reread"), (16, 3, "slow+skip")])
+def test_gated_big_rounds(n, d, pattern, dev):
+    """Big rounds are pre-enqueued: the fold of round i waits on the GPU for its challenge (sumcheck.hip
+    gate_open) while round i's messages are read. A host slower than the fold's bounded wait
+    ("slow": the fold ends and the host relaunches the round), unrelated kernels queued on the
+    prover's stream behind a waiting fold ("busy"), rounds whose messages are never read ("skip":
+    the pre-enqueued messages assumed a derived p(1) and are cancelled) and rounds read twice
+    ("reread") must all give the oracle's transcript word for word."""
+    import time
+
+    import torch
+    ev, ch = _case(n, d, 8080 + n + d)
+    bs = O.bitslice128(ev)
+    want_s, want_p = O.sumcheck_run(bs, n, d, 1, ch)
+    sc = B.Sumcheck(n, d, True, bs)
+    ps = torch.cuda.ExternalStream(sc.stream_handle(), device=dev)
+    junk = torch.ones(1 << 20, device=dev)
+    for r in range(n + 1):
+        if not ("skip" in pattern and r % 3 == 1 and r < n):
+            s, p = sc.this_round_messages()
+            assert np.array_equal(s, want_s[r]), "round %d sum" % r
+            assert np.array_equal(p, want_p[r]), "round %d points" % r
+            if pattern == "reread":
+                s2, p2 = sc.this_round_messages()
+                assert np.array_equal(s2, s) and np.array_equal(p2, p), "round %d re-read" % r
+        if pattern == "busy":
+            with torch.cuda.stream(ps):
+                junk.mul_(1.5).add_(-0.5)
+            ps.synchronize()
+        if "slow" in pattern and r % 2 == 0:
+            time.sleep(0.002)  # 2 ms: ten times the gated fold's wait
+        if r < n:
+            sc.move_to_next_round(ch[r])
+    sc.close()
+
+
+def test_gated_round_abandoned_prover(dev):
+    """A prover destroyed while a pre-enqueued fold waits for its challenge cancels it: the stream
+    drains at once and the next prover's transcript is the oracle's."""
+    import time
+
+    import torch
+    n, d = 16, 3
+    ev, ch = _case(n, d, 9090)
+    bs = O.bitslice128(ev)
+    sc = B.Sumcheck(n, d, True, bs)
+    for r in range(3):
+        sc.this_round_messages()
+        sc.move_to_next_round(ch[r])
+    sc.this_round_messages()  # round 3 read; round 3's fold waits for its challenge
+    t0 = time.perf_counter()
+    sc.close()
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 < 5.0
+    want_s, want_p = O.sumcheck_run(bs, n, d, 1, ch)
+    sc = B.Sumcheck(n, d, True, bs)
+    got_s, got_p = _transcript(sc, n, ch)
+    sc.close()
+    assert np.array_equal(got_s, want_s) and np.array_equal(got_p, want_p)
