@@ -117,87 +117,11 @@ struct ScArgs {
 	uint32_t* sink;     // optional device copy of the raw point words + flags (bn_sumcheck_set_message_sink)
 	uint32_t seq;       // this launch's sequence number
 	int post;           // 1: the last workgroup posts the points (small grids), 0: sc_post does
-	// pre-enqueued ("gated") big rounds: the fold is queued before the host has the challenge and
-	// waits for it on the GPU (gated 1). The messages queued behind it (gated 2) always run, but post
-	// only if the fold folded; when it timed out, the host relaunches the round (wait_posted).
-	int gated;
-	uint32_t gate_ticket;
-	uint32_t* gate;       // device: [0] decision (ticket, or ticket | kGateAbort), [1..4] challenge
-	uint32_t* gate_host;  // host-mapped slot of this ticket's parity (kGateR, kGateTicket, kGateExit, kGateDecision)
 	uint32_t kcol[kMaxD + 1][4];  // GF(2^4) products k * 2^a (interpolation point k)
 	int dbg;  // development build (BN_DEV) only: BN_SC_DBG bit 0 = synthetic operands instead of
 	          // column loads, bit 1 = no products, bit 2 = no k-multiples, bit 3 = no parity
 	          // reduction (wrong results; for timing experiments)
 };
-
-constexpr uint32_t kGateAbort = 0x80000000u;
-constexpr uint32_t kGateBroken = 0xFFFFFFFFu;                   // kGateExit: a workgroup lost the decision
-// host-mapped words per ticket parity (two consecutive gated rounds never share a slot): the
-// challenge, the ticket the host released (or ticket | kGateAbort), the ticket of a fold that timed
-// out, and the fold's decision
-constexpr int kGateR = 0, kGateTicket = 4, kGateExit = 5, kGateDecision = 6, kGateSlot = 8;
-constexpr unsigned long long kGateTimeoutTicks = 20000ull;       // 200 us at 100 MHz (s_memrealtime)
-constexpr unsigned long long kGateLostTicks = 1000000ull;        // 10 ms: the deciding workgroup never decided
-
-// Prologue of a gated fold. Workgroup 0 (dispatched first) waits for the host to release this
-// round's ticket (or abort it) for at most kGateTimeoutTicks, publishes the decision and the
-// challenge in device memory, and on a timeout tells the host, which relaunches the round. The
-// other workgroups wait for that decision. Returns true with the challenge in sh[1..4] (LDS) when
-// the fold may run.
-// Every access here is a relaxed atomic that bypasses the caches (sc1: device-coherent, sc0 sc1:
-// system) and the stores are ordered by waiting for their completion: acquire / release at agent
-// or system scope would invalidate or write back the whole L2 of the XCD, in every polling
-// iteration and in every workgroup (measured: the gated rounds ran 20-60 us slower per round).
-__device__ __forceinline__ uint32_t ld_dev(const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
-__device__ __forceinline__ void st_dev(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
-__device__ __forceinline__ void mem_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-__device__ __forceinline__ bool gate_open(const ScArgs& A, uint32_t* sh) {
-	if (threadIdx.x == 0) {
-		uint32_t v;
-		const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-		if (blockIdx.x == 0) {
-			bool timed_out = false;
-			for (;;) {
-				v = ld_sys(A.gate_host + kGateTicket);
-				if (v == A.gate_ticket || v == (A.gate_ticket | kGateAbort)) break;
-				if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) {
-					timed_out = true;
-					v = A.gate_ticket | kGateAbort;
-					break;
-				}
-				__builtin_amdgcn_s_sleep(2);
-			}
-			mem_done();  // the challenge is read after the ticket (the host wrote it first)
-			if (v == A.gate_ticket)
-				for (int i = 0; i < 4; i++) st_dev(A.gate + 1 + i, ld_sys(A.gate_host + kGateR + i));
-			mem_done();  // the challenge is in device memory before the decision
-			st_dev(A.gate, v);
-			if (timed_out) st_sys(A.gate_host + kGateExit, A.gate_ticket);
-			st_sys(A.gate_host + kGateDecision, v);
-		} else {
-			for (;;) {
-				v = ld_dev(A.gate);
-				if (v == A.gate_ticket || v == (A.gate_ticket | kGateAbort)) break;
-				if (__builtin_amdgcn_s_memrealtime() - t0 > kGateLostTicks) {
-					// cannot happen while workgroup 0 runs first; if it ever does, the host fails loudly
-					st_sys(A.gate_host + kGateExit, kGateBroken);
-					v = A.gate_ticket | kGateAbort;
-					break;
-				}
-				__builtin_amdgcn_s_sleep(2);
-			}
-		}
-		mem_done();
-		sh[0] = v;
-		if (v == A.gate_ticket)
-			for (int i = 0; i < 4; i++) sh[1 + i] = ld_dev(A.gate + 1 + i);
-	}
-	__syncthreads();
-	return sh[0] == A.gate_ticket;
-}
 
 // lo/hi limbs of column j for pair p (this lane's limb l)
 template <int MODE>
@@ -239,16 +163,8 @@ __device__ __forceinline__ void load_pair(const ScArgs& A, int j, size_t p, int 
 	}
 }
 
-// Messages queued behind a gated fold that did not fold (timed out or cancelled) ran on unfolded
-// columns: they must not post (the host relaunches the round, or has moved on). The fold kernel
-// ended before this one started, so its decision is in device memory; uniform per workgroup.
-__device__ __forceinline__ bool post_blocked(const ScArgs& A) {
-	return A.gated == 2 && __hip_atomic_load(A.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != A.gate_ticket;
-}
-
 // Reduce the accumulator copies and post the points + sequence word to host-mapped memory.
 __device__ __forceinline__ void post_points(const ScArgs& A, int t) {
-	if (post_blocked(A)) return;
 	if (t < 4 * (A.kmax + 1)) {
 		uint32_t v = 0;
 		for (int c = 0; c < kAccCopies; c++)
@@ -361,7 +277,6 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_messages(ScArgs A) {
 			atomicXor(A.acc + (blockIdx.x % kAccCopies) * kAccStride + threadIdx.x, accL[threadIdx.x]);
 		return;  // sc_post follows
 	}
-	if (post_blocked(A)) return;
 	if (gridDim.x == 1) {  // a single workgroup posts its own sums
 		if (threadIdx.x < 4 * (A.kmax + 1)) {
 			A.res[threadIdx.x] = accL[threadIdx.x];
@@ -416,25 +331,16 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold(ScArgs A) {
 	const int l = threadIdx.x % G, qw = threadIdx.x / G;
 	const Slot S{lds + qw * Grp<G>::kSlotWords};
 	uint32_t* R = lds + Grp<G>::kSlotsWords;  // the challenge, broadcast-bitsliced, shared
+	if (threadIdx.x < 128) R[threadIdx.x] = 0u - ((A.r[threadIdx.x / 32] >> (threadIdx.x % 32)) & 1u);
+	__syncthreads();
 	const size_t items = (size_t)A.d * A.n_pairs;
 	const size_t it = (size_t)blockIdx.x * Grp<G>::kGroups + qw;
-	const int j = (int)(it / A.n_pairs);
-	const size_t p = it % A.n_pairs;
-	uint32_t lo[32], hi[32], emask = 0;
-	// the item's loads are issued before a gated fold's wait for its challenge, so they overlap
-	if (it < items && l < 4) load_pair<MODE>(A, j, p, l, lo, hi, emask);
-	// (no pointer to A.r: the address of a kernel argument puts the whole ScArgs on the stack)
-	uint32_t rw = 0;
-	if (A.gated == 1) {
-		if (!gate_open(A, R + 128)) return;
-		if (threadIdx.x < 128) rw = R[129 + threadIdx.x / 32];
-	} else if (threadIdx.x < 128) {
-		rw = A.r[threadIdx.x / 32];
-	}
-	if (threadIdx.x < 128) R[threadIdx.x] = 0u - ((rw >> (threadIdx.x % 32)) & 1u);
-	__syncthreads();
 	if (it < items) {  // one item per group (no grid-stride loop: it costs registers)
+		const int j = (int)(it / A.n_pairs);
+		const size_t p = it % A.n_pairs;
+		uint32_t lo[32], hi[32], emask;
 		if (l < 4) {
+			load_pair<MODE>(A, j, p, l, lo, hi, emask);
 #pragma unroll
 			for (int i = 0; i < 32; i++) hi[i] ^= lo[i];
 			sst(S, l, hi);
@@ -471,35 +377,19 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_coal(ScArgs A) {
 	const Slot S{lds + qw * kQuadWords};
 	uint32_t* wslots = lds + (qw & ~15) * kQuadWords;
 	uint32_t* R = lds + kQuadsPerWG * kQuadWords;
+	if (threadIdx.x < 128) R[threadIdx.x] = 0u - ((A.r[threadIdx.x / 32] >> (threadIdx.x % 32)) & 1u);
+	__syncthreads();
 	const size_t it0 = (size_t)blockIdx.x * kQuadsPerWG + (qw & ~15);  // the wave's first item
-	const bool active = it0 < (size_t)A.d * A.n_pairs;
+	if (it0 >= (size_t)A.d * A.n_pairs) return;
 	const int j = (int)(it0 / A.n_pairs);
 	const size_t p0 = it0 % A.n_pairs;
 	uint32_t* lo = A.cols + (size_t)j * A.col_stride + 128 * p0;
 	const uint32_t* hi = lo + 128 * A.hb;
-	// the wave's loads are issued before a gated fold's wait for its challenge, so they overlap
-	uint4 a[8], b[8];
-	if (active) {
 #pragma unroll
-		for (int i = 0; i < 8; i++) {
-			a[i] = *(const uint4*)(lo + 4 * lane + 256 * i);
-			b[i] = *(const uint4*)(hi + 4 * lane + 256 * i);
-		}
+	for (int i = 0; i < 8; i++) {
+		const uint4 a = *(const uint4*)(lo + 4 * lane + 256 * i), b = *(const uint4*)(hi + 4 * lane + 256 * i);
+		*(uint4*)coal_addr(wslots, lane, i) = make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
 	}
-	// (no pointer to A.r: the address of a kernel argument puts the whole ScArgs on the stack)
-	uint32_t rw = 0;
-	if (A.gated == 1) {
-		if (!gate_open(A, R + 128)) return;
-		if (threadIdx.x < 128) rw = R[129 + threadIdx.x / 32];
-	} else if (threadIdx.x < 128) {
-		rw = A.r[threadIdx.x / 32];
-	}
-	if (threadIdx.x < 128) R[threadIdx.x] = 0u - ((rw >> (threadIdx.x % 32)) & 1u);
-	__syncthreads();
-	if (!active) return;
-#pragma unroll
-	for (int i = 0; i < 8; i++)
-		*(uint4*)coal_addr(wslots, lane, i) = make_uint4(a[i].x ^ b[i].x, a[i].y ^ b[i].y, a[i].z ^ b[i].z, a[i].w ^ b[i].w);
 #ifdef BN_DEV
 	if (!(A.dbg & 2))
 #endif
@@ -783,24 +673,6 @@ struct bn_sumcheck {
 	unsigned long long* h_trace = nullptr;  // development build (BN_SC_TIMING): the server's phase stamps
 	double t_post = 0;                      // ... and the host's time of the last challenge post
 	bool read_this_round = false;
-	// Pre-enqueued big rounds (gated folds). When round i's messages are queued, the fold of round i
-	// (waiting on the GPU for its challenge) and the messages of round i + 1 are queued behind them;
-	// move_to_next_round then only writes the challenge into host-mapped words, so neither the fold's
-	// launch nor its dispatch sits between the host's challenge and the GPU. A gated fold that gets
-	// no challenge within kGateTimeoutTicks ends without folding, and the host relaunches the round.
-	struct Gate {
-		bool valid = false;
-		uint32_t ticket = 0, seq = 0;
-		int skip1 = 0;
-		size_t cur = 0;  // evaluations per column before the fold
-		uint32_t r[4] = {0, 0, 0, 0};
-	};
-	Gate gate_pending;   // queued, waiting for its challenge
-	Gate gate_released;  // challenge written; its messages not read yet (it may still time out)
-	uint32_t* h_gate = nullptr;  // host-mapped: two slots of kGateSlot words (by ticket parity)
-	uint32_t* d_gate = nullptr;  // device: [0] decision, [1..4] challenge
-	uint32_t gate_tickets = 0;
-	bool gates = true;  // BN_SC_GATE=0 (development build): every fold launched after its challenge
 };
 
 namespace {
@@ -808,30 +680,20 @@ namespace {
 using namespace bn;
 using namespace bn::quad;
 
-// A launch of a gated round (sc_launch's defaults take everything from the prover's state)
-struct LaunchGate {
-	int gated = 0;          // 1: gated fold, 2: messages behind one (they post only if it folded)
-	uint32_t ticket = 0;
-	size_t cur = 0;         // evaluations per column (0: sc->cur)
-	int skip1 = -1;         // messages: skip p(1) (-1: from the claim state)
-	uint32_t seq = 0;       // messages: sequence number (0: ++sc->seq)
-};
-
-int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r, const LaunchGate* g = nullptr) {
+int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 	ScArgs A{};
 	A.cols = sc->cols;
 	A.col_stride = sc->col_words;
 	A.d = sc->d;
-	const size_t cur = g && g->cur ? g->cur : sc->cur;
-	if (cur >= 64) {
+	if (sc->cur >= 64) {
 		A.mode = 0;
-		A.n_pairs = cur / 64;
-		A.hb = cur / 64;
+		A.n_pairs = sc->cur / 64;
+		A.hb = sc->cur / 64;
 		A.kmax = sc->d;
-	} else if (cur >= 2) {
+	} else if (sc->cur >= 2) {
 		A.mode = 1;
 		A.n_pairs = 1;
-		A.h = (int)(cur / 2);
+		A.h = (int)(sc->cur / 2);
 		A.kmax = sc->d;
 	} else {
 		A.mode = 2;
@@ -839,21 +701,12 @@ int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r, const LaunchGate* g
 		A.kmax = 0;
 	}
 	A.skip1 = (!fold && (sc->have_claim || sc->claim_pending) && A.mode != 2) ? 1 : 0;
-	if (g && g->skip1 >= 0 && !fold) A.skip1 = A.mode != 2 ? g->skip1 : 0;
 	A.res = sc->d_res;
 	A.sink = fold ? nullptr : sc->sink;
-	if (!fold) A.seq = g && g->seq ? g->seq : ++sc->seq;
-	if (g && g->gated) {
-		A.gated = g->gated;
-		A.gate_ticket = g->ticket;
-		A.gate = sc->d_gate;
-		uint32_t* dh = nullptr;
-		BN_HIP(hipHostGetDevicePointer((void**)&dh, sc->h_gate, 0));
-		A.gate_host = dh + kGateSlot * (g->ticket & 1);
-	}
+	if (!fold) A.seq = ++sc->seq;
 	A.acc = sc->acc + kAccSet * sc->par;
 	A.clr = sc->acc + kAccSet * (1 - sc->par);
-	if (fold && r) memcpy(A.r, r, 16);
+	if (fold) memcpy(A.r, r, 16);
 #ifdef BN_DEV
 	{
 		static const int dbg = getenv("BN_SC_DBG") ? atoi(getenv("BN_SC_DBG")) : 0;
@@ -963,108 +816,9 @@ void server_post(bn_sumcheck* sc, const uint32_t* r, bool skip1) {
 #endif
 }
 
-// ---- pre-enqueued (gated) big rounds
-
-int queue_messages(bn_sumcheck* sc);
-
-// The fold of the round whose messages were just queued (sc->cur evaluations) can be queued ahead
-// of its challenge: an unsharded, eager prover without a message sink, a mode-0 fold, and the
-// round after it still launched (not served by sc_server)
-bool gate_eligible(const bn_sumcheck* sc) {
-	return sc->gates && sc->eager && sc->world == 1 && !sc->sink && sc->prepared && !sc->server && sc->msgs_queued &&
-	       !sc->gate_pending.valid && sc->cur >= 128 && sc->cur / 2 > sc->server_max_cur;
-}
-
-// queue the gated fold of this round and the next round's messages behind it
-int gate_enqueue(bn_sumcheck* sc) {
-	bn_sumcheck::Gate& g = sc->gate_pending;
-	g.ticket = ++sc->gate_tickets & ~kGateAbort;
-	if (g.ticket == 0) g.ticket = sc->gate_tickets = 1;
-	g.cur = sc->cur;
-	g.seq = sc->seq + 1;
-	// the messages assume the caller reads this round through bn_sumcheck_round_messages, so the
-	// next round's claim is derived (checked at release: otherwise the gate is cancelled)
-	g.skip1 = sc->derive_p1 ? 1 : 0;
-	LaunchGate lf;
-	lf.gated = 1;
-	lf.ticket = g.ticket;
-	lf.cur = g.cur;
-	int rc = sc_launch(sc, true, nullptr, &lf);
-	if (rc != BN_OK) return rc;
-	LaunchGate lm;
-	lm.gated = 2;
-	lm.ticket = g.ticket;
-	lm.cur = g.cur / 2;
-	lm.skip1 = g.skip1;
-	lm.seq = g.seq;
-	rc = sc_launch(sc, false, nullptr, &lm);
-	if (rc != BN_OK) return rc;
-	sc->par ^= 1;
-	g.valid = true;
-	return BN_OK;
-}
-
-volatile uint32_t* gate_slot(bn_sumcheck* sc, uint32_t ticket) {
-	return (volatile uint32_t*)sc->h_gate + kGateSlot * (ticket & 1);
-}
-
-void gate_write_ticket(bn_sumcheck* sc, uint32_t ticket, uint32_t v) {
-	std::atomic_thread_fence(std::memory_order_release);
-	gate_slot(sc, ticket)[kGateTicket] = v;
-}
-
-// Abort the pending gated round: its fold ends without folding; the messages queued behind it
-// still run (on unfolded columns) and post their sequence number, so later launches use higher ones.
-// They also used one accumulator set and cleared the other, which the next launch uses: the sets
-// keep alternating, so nothing is restored.
-void gate_cancel(bn_sumcheck* sc) {
-	if (!sc->gate_pending.valid) return;
-	gate_write_ticket(sc, sc->gate_pending.ticket, sc->gate_pending.ticket | kGateAbort);
-	if ((int32_t)(sc->gate_pending.seq - sc->seq) > 0) sc->seq = sc->gate_pending.seq;
-	sc->gate_pending.valid = false;
-}
-
-// A released gated fold that timed out before its challenge arrived: cancel whatever was queued
-// behind it and launch its fold and its messages again
-int gate_relaunch(bn_sumcheck* sc) {
-	bn_sumcheck::Gate q = sc->gate_released;
-	sc->gate_released.valid = false;
-	gate_cancel(sc);
-	LaunchGate lf;
-	lf.cur = q.cur;
-	int rc = sc_launch(sc, true, q.r, &lf);
-	if (rc != BN_OK) return rc;
-	return queue_messages(sc);
-}
-
-// Before anything but the reading of its messages follows a released gated fold: wait until the
-// fold has decided (it may not have reached the GPU yet) and relaunch it if it timed out
-int gate_settle(bn_sumcheck* sc) {
-	gate_cancel(sc);
-	if (!sc->gate_released.valid) return BN_OK;
-	const uint32_t t = sc->gate_released.ticket;
-	volatile uint32_t* slot = gate_slot(sc, t);
-	for (;;) {
-		const uint32_t v = slot[kGateDecision];
-		if (slot[kGateExit] == kGateBroken) BN_FAIL(BN_ERR_HIP, "gated fold: a workgroup never saw the decision");
-		if (v == t) {
-			sc->gate_released.valid = false;
-			return BN_OK;
-		}
-		if (v == (t | kGateAbort)) {
-			std::atomic_thread_fence(std::memory_order_acquire);
-			return gate_relaunch(sc);
-		}
-		const hipError_t e = hipStreamQuery(sc->stream);
-		if (e != hipSuccess && e != hipErrorNotReady) BN_FAIL(BN_ERR_HIP, "gated fold: %s", hipGetErrorString(e));
-		if (e == hipSuccess && slot[kGateDecision] != t && slot[kGateDecision] != (t | kGateAbort))
-			BN_FAIL(BN_ERR_HIP, "gated fold %u ended without a decision", t);
-	}
-}
-
 // Wait for the round's posted sequence number (the stream is queried between polls, so a failed
-// kernel is reported rather than waited for); relaunches a round server, or a gated fold, that
-// timed out before taking this round's challenge.
+// kernel is reported rather than waited for); relaunches a round server that timed out before
+// taking this round's challenge.
 int wait_posted(bn_sumcheck* sc) {
 	const volatile uint32_t* posted = sc->h_res + kResSeq;
 	for (;;) {
@@ -1080,16 +834,6 @@ int wait_posted(bn_sumcheck* sc) {
 			}
 #endif
 			return BN_OK;
-		}
-		if (sc->gate_released.valid) {
-			const uint32_t ex = gate_slot(sc, sc->gate_released.ticket)[kGateExit];
-			if (ex == kGateBroken) BN_FAIL(BN_ERR_HIP, "gated fold: a workgroup never saw the decision");
-			if (ex == sc->gate_released.ticket) {
-				std::atomic_thread_fence(std::memory_order_acquire);
-				const int grc = gate_relaunch(sc);
-				if (grc != BN_OK) return grc;
-				continue;
-			}
 		}
 		if (sc->server && ((volatile uint32_t*)sc->h_ctl)[kCtlExit] == sc->ticket - 1) {
 			// the challenge and the ticket are already posted: the new server folds 2 cur down to cur
@@ -1130,13 +874,6 @@ int sc_common_init(bn_sumcheck* sc) {
 	BN_HIP(hipHostGetDevicePointer((void**)&sc->d_res, sc->h_res, 0));
 	BN_HIP(hipHostMalloc((void**)&sc->h_ctl, sizeof(uint32_t) * kCtlWords, hipHostMallocMapped | hipHostMallocCoherent));
 	memset(sc->h_ctl, 0, sizeof(uint32_t) * kCtlWords);
-	BN_HIP(hipHostMalloc((void**)&sc->h_gate, sizeof(uint32_t) * 2 * kGateSlot, hipHostMallocMapped | hipHostMallocCoherent));
-	memset(sc->h_gate, 0, sizeof(uint32_t) * 2 * kGateSlot);
-	BN_HIP(hipMalloc(&sc->d_gate, sizeof(uint32_t) * 8));
-	BN_HIP(hipMemsetAsync(sc->d_gate, 0, sizeof(uint32_t) * 8, sc->stream));
-#ifdef BN_DEV
-	if (const char* e = getenv("BN_SC_GATE")) sc->gates = atoi(e) != 0;
-#endif
 	BN_HIP(hipFuncSetAttribute((const void*)sc_server, hipFuncAttributeMaxDynamicSharedMemorySize, (int)srv_lds_bytes()));
 #ifdef BN_DEV
 	if (const char* e = getenv("BN_SC_SERVER_MAX_CUR")) sc->server_max_cur = (size_t)atol(e);
@@ -1158,14 +895,11 @@ void sc_free(bn_sumcheck* sc) {
 		std::atomic_thread_fence(std::memory_order_release);
 		((volatile uint32_t*)sc->h_ctl)[kCtlTicket] = kSrvStop;
 	}
-	if (sc->h_gate) gate_cancel(sc);  // a gated fold still waiting for its challenge ends at once
 	if (sc->stream) (void)hipStreamSynchronize(sc->stream);
 	if (sc->cols) (void)hipFree(sc->cols);
 	if (sc->acc) (void)hipFree(sc->acc);
 	if (sc->h_res) (void)hipHostFree(sc->h_res);
 	if (sc->h_ctl) (void)hipHostFree(sc->h_ctl);
-	if (sc->h_gate) (void)hipHostFree(sc->h_gate);
-	if (sc->d_gate) (void)hipFree(sc->d_gate);
 	if (sc->h_trace) (void)hipHostFree(sc->h_trace);
 	if (sc->stream) (void)hipStreamDestroy(sc->stream);
 	delete sc;
@@ -1452,11 +1186,6 @@ extern "C" int bn_sumcheck_import_gathered(bn_sumcheck* sc, const uint32_t* word
 
 extern "C" int bn_sumcheck_set_message_sink(bn_sumcheck* sc, void* d_words) {
 	BN_CHECK_ARG(sc, "NULL prover");
-	DeviceScope ds(sc->device);
-	const int rc = gate_settle(sc);
-	if (rc != BN_OK) return rc;
-	// queued messages were launched without (or with another) sink: the next read queues them again
-	sc->msgs_queued = false;
 	sc->sink = (uint32_t*)d_words;
 	return BN_OK;
 }
@@ -1484,11 +1213,8 @@ extern "C" int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32
 		return BN_OK;
 	}
 	if (!sc->msgs_queued) {
-		// a second read of this round: its messages again (a gated fold queued for the next round would
-		// hold them back: cancel it)
-		int rc = gate_settle(sc);
+		int rc = queue_messages(sc);
 		if (rc != BN_OK) return rc;
-		if (!sc->msgs_queued && (rc = queue_messages(sc)) != BN_OK) return rc;
 	}
 	sc->msgs_queued = false;
 	int rc = BN_OK;
@@ -1502,7 +1228,6 @@ extern "C" int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32
 	}
 	if ((rc = wait_posted(sc)) != BN_OK) return rc;
 	std::atomic_thread_fence(std::memory_order_acquire);
-	sc->gate_released.valid = false;  // its messages are posted, so it folded
 	const int npts = sc->d + 1;
 	uint32_t acc[4 * (kMaxD + 1)];
 	for (int i = 0; i < 4 * npts; i++) acc[i] = ((const volatile uint32_t*)sc->h_res)[i];
@@ -1565,31 +1290,7 @@ extern "C" int bn_sumcheck_move_to_next_round(bn_sumcheck* sc, const uint32_t* c
 		if (prc != BN_OK) return prc;
 	}
 	const bool to_server = sc->server || server_eligible(sc);
-	// a released gated fold whose messages were not read: make sure it folded before moving on
-	// (this cancels the pending gated round too; it is launched the ordinary way below)
-	if (sc->gate_released.valid) {
-		const int src = gate_settle(sc);
-		if (src != BN_OK) return src;
-	}
-	bool released = false;
-	if (sc->gate_pending.valid) {
-		// this round's fold is queued and waits for its challenge: release it, if the messages queued
-		// behind it made the assumption that holds now (p(1) derived from this round's points)
-		const int want = (sc->have_pts && sc->derive_p1) ? 1 : 0;
-		if (!to_server && sc->gate_pending.cur == sc->cur && sc->gate_pending.skip1 == want) {
-			bn_sumcheck::Gate& g = sc->gate_pending;
-			volatile uint32_t* slot = gate_slot(sc, g.ticket);
-			for (int i = 0; i < 4; i++) slot[kGateR + i] = challenge[i];
-			gate_write_ticket(sc, g.ticket, g.ticket);
-			memcpy(g.r, challenge, 16);
-			sc->gate_released = g;
-			g.valid = false;
-			released = true;
-		} else {
-			gate_cancel(sc);
-		}
-	}
-	if (!to_server && !released) {
+	if (!to_server) {
 		int rc = sc_launch(sc, true, challenge);
 		if (rc != BN_OK) return rc;
 	}
@@ -1622,17 +1323,8 @@ extern "C" int bn_sumcheck_move_to_next_round(bn_sumcheck* sc, const uint32_t* c
 	sc->cur /= 2;
 	sc->round++;
 	sc->sharded_used = true;
-	if (released) {
-		sc->seq = sc->gate_released.seq;  // the gated messages post this sequence number
-		sc->msgs_queued = true;
-	} else {
-		sc->msgs_queued = false;  // a queued, unread messages kernel ran before the fold: dropped
-		if (sc->eager && !(sc->world > 1 && sc->cur <= 32)) {
-			const int rc = queue_messages(sc);
-			if (rc != BN_OK) return rc;
-		}
-	}
-	if (gate_eligible(sc)) return gate_enqueue(sc);
+	sc->msgs_queued = false;  // a queued, unread messages kernel ran before the fold: dropped
+	if (sc->eager && !(sc->world > 1 && sc->cur <= 32)) return queue_messages(sc);
 	return BN_OK;
 }
 
