@@ -911,7 +911,7 @@ const BsPass* bs_passes(bn_antt_plan* plan, size_t* n_passes) {
 }
 
 struct BsDevKnobs {
-	int pf_mode = 0, dbg = 0, stop_stage = -1, split = -1, mid_pf = -1;
+	int pf_mode = 0, dbg = 0, stop_stage = -1, split = -1, mid_pf = -1, rr_last = -1;
 	bool persist = true, trace = false;
 	size_t max_passes = ~(size_t)0;
 };
@@ -930,6 +930,7 @@ static BsDevKnobs dev_knobs() {
 	if (const char* e = getenv("BN_DEBUG_STOP_STAGE")) k.stop_stage = atoi(e);
 	if (const char* e = getenv("BN_SPLIT")) k.split = atoi(e);  // 0: never lane-split, 1: always
 	if (const char* e = getenv("BN_MID_PF")) k.mid_pf = atoi(e);  // 1: middle passes on antt_rr_mid_pf
+	if (const char* e = getenv("BN_RR_LAST")) k.rr_last = atoi(e);  // 0: small bottom passes on LDS tiles
 	k.trace = getenv("BN_TRACE") != nullptr;
 #endif
 	return k;
@@ -962,11 +963,21 @@ static bool use_split(const bn_antt_plan* plan, const BsPass& pass, size_t ntile
 	return ntiles < (size_t)2 * (size_t)plan->num_cus;
 }
 
+// Bottom pass of a small launch (fewer tiles than two per CU: one wave per SIMD either way) on
+// register tiles, compiled without the three-waves bound (antt_rr.hip small_last): C3 (one 2^20
+// transform) 0.0800-0.0802 vs 0.0822-0.0824 ms on LDS tiles (round 5, tools/r05_c3_rrlast.sh).
+// BN_RR_LAST=0 (development build) keeps it on LDS tiles.
+static bool use_rr_last(const bn_antt_plan* plan, const BsPass& pass, size_t ntiles, const BsDevKnobs& kn) {
+	if (kn.rr_last == 0 || plan->variant != 5 || plan->limbs != 4 || pass.role != ROLE_LAST) return false;
+	return ntiles < (size_t)2 * (size_t)plan->num_cus;
+}
+
 static int launch_one(bn_antt_plan* plan, const BsPass& pass, int i, const uint32_t* d_in, uint32_t* d_out,
                       size_t batch, hipStream_t st, const BsDevKnobs& kn) {
 	// variant 4: every pass on register tiles; variant 5 (mixed): register tiles for the passes whose
 	// twiddles all lie in GF(2^8) (their kernel fits four waves per SIMD), LDS tiles for the others
 	if (plan->variant == 4 || (plan->variant == 5 && pass_fmax(pass) <= 8)) return rr_launch_pass(plan, i, d_in, d_out, batch, st);
+	if (use_rr_last(plan, pass, (batch << plan->log_rate) << pass.n_outer, kn)) return rr_launch_pass(plan, i, d_in, d_out, batch, st);
 	const int L = plan->limbs;
 	BsParams prm;
 	prm.src = d_in;
@@ -1056,6 +1067,7 @@ const void* bs_pass_kernel(bn_antt_plan* plan, int i) {
 #ifdef BN_DEV
 	if (use_mid_pf(plan, pass, ntiles, kn)) return rr_mid_pf_kernel(pass);
 #endif
+	if (use_rr_last(plan, pass, ntiles, kn)) return rr_pass_kernel(plan, pass);
 	if (use_split(plan, pass, ntiles, kn)) return split_kernel_for(pass.role);
 	const bool pf = kn.persist && (kn.pf_mode == 2 || (kn.pf_mode == 1 && fmax <= 8));
 	return kernel_for(plan->limbs, pass.role, fmax, pf);

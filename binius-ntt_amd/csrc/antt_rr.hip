@@ -117,8 +117,8 @@ __device__ __forceinline__ void fma_tw(int field, uint32_t tw, const uint32_t* v
 	}
 }
 
-template <int L, int ROLE, int FMAX>
-__global__ __launch_bounds__(64 * L, RrOcc<ROLE>::value) void antt_rr_pass(RrParams P) {
+template <int L, int ROLE, int FMAX, int OCC = RrOcc<ROLE>::value>
+__global__ __launch_bounds__(64 * L, OCC) void antt_rr_pass(RrParams P) {
 	extern __shared__ uint32_t lds[];
 	constexpr bool IN_COMPACT = ROLE == ROLE_FIRST || ROLE == ROLE_SINGLE;
 	constexpr bool LAST = ROLE == ROLE_LAST || ROLE == ROLE_SINGLE;
@@ -541,6 +541,15 @@ static const void* kernel_for(int L, int role, int fmax) {
 	if (L == 4) return fmax <= 8 ? kernel_f<4, 8>(role) : fmax <= 16 ? kernel_f<4, 16>(role) : kernel_f<4, 32>(role);
 	return fmax <= 8 ? kernel_f<1, 8>(role) : fmax <= 16 ? kernel_f<1, 16>(role) : kernel_f<1, 32>(role);
 }
+// The bottom pass of a launch with fewer tiles than two per CU runs one wave per SIMD whatever its
+// register count, so it is compiled without the three-waves bound (no spills)
+static bool small_last(int L, int role, size_t ntiles, int num_cus) {
+	return L == 4 && role == ROLE_LAST && ntiles < (size_t)2 * (size_t)num_cus;
+}
+static const void* kernel_small_last(int fmax) {
+	return fmax <= 8 ? (const void*)antt_rr_pass<4, ROLE_LAST, 8, 1> : fmax <= 16 ? (const void*)antt_rr_pass<4, ROLE_LAST, 16, 1>
+	                                                                              : (const void*)antt_rr_pass<4, ROLE_LAST, 32, 1>;
+}
 // every role stages through LDS: compact elements (first / last pass) or coalesced bitsliced lines
 static size_t lds_bytes(int L, int role) {
 	(void)role;
@@ -560,10 +569,15 @@ int rr_prepare(bn_antt_plan* plan) {
 			for (int f : {8, 16, 32})
 				BN_HIP(hipFuncSetAttribute(rr::kernel_for(L, role, f), hipFuncAttributeMaxDynamicSharedMemorySize,
 				                           (int)std::max<size_t>(rr::lds_bytes(L, role), 1)));
+	for (int f : {8, 16, 32})
+		BN_HIP(hipFuncSetAttribute(rr::kernel_small_last(f), hipFuncAttributeMaxDynamicSharedMemorySize,
+		                           (int)rr::lds_bytes(4, ROLE_LAST)));
 	return BN_OK;
 }
 
 const void* rr_pass_kernel(bn_antt_plan* plan, const BsPass& pass) {
+	const size_t ntiles = ((size_t)1 << plan->log_rate) << pass.n_outer;  // one transform (see bs_pass_kernel)
+	if (rr::small_last(plan->limbs, pass.role, ntiles, plan->num_cus)) return rr::kernel_small_last(pass_fmax(pass));
 	return rr::kernel_for(plan->limbs, pass.role, pass_fmax(pass));
 }
 
@@ -591,8 +605,9 @@ int rr_launch_pass(bn_antt_plan* plan, int i, const uint32_t* d_in, uint32_t* d_
 	rc = timing_begin(plan, i, st);
 	if (rc != BN_OK) return rc;
 	void* args[] = {&prm};
-	BN_HIP(hipLaunchKernel(rr::kernel_for(L, pass.role, pass_fmax(pass)), dim3((unsigned)ntiles), dim3(64 * L), args,
-	                       rr::lds_bytes(L, pass.role), st));
+	const void* k = rr::small_last(L, pass.role, ntiles, plan->num_cus) ? rr::kernel_small_last(pass_fmax(pass))
+	                                                                    : rr::kernel_for(L, pass.role, pass_fmax(pass));
+	BN_HIP(hipLaunchKernel(k, dim3((unsigned)ntiles), dim3(64 * L), args, rr::lds_bytes(L, pass.role), st));
 	return timing_end(plan, i, st);
 }
 
