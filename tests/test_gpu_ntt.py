@@ -214,6 +214,11 @@ def test_lane_split_passes_gf128(ntt_md5, log_h, r, dev):
     if log_h >= 17:
         assert any("antt_bs3_pass" in n for n in names), names
         assert "antt_bs3_pass" not in names[-1], names  # the bottom pass keeps one wave per limb
+    if len(names) > 1 and (1 << (log_h + r - 12)) < 2 * 256:
+        # ... and, fewer than two tiles per CU, runs on register tiles compiled for one wave per SIMD
+        # (round 5: no spills)
+        import re
+        assert re.search(r"antt_rr_pass<4, 2, \d+, 1>", names[-1]), names
     y = _run_device(ntt, x.reshape(-1), dev).reshape(-1, 4)
     assert np.array_equal(y, O.antt128(x, log_h, r))
     if r == 0:
