@@ -53,8 +53,34 @@ public:
 		ulvt::bn_check(bn_sumcheck_move_to_next_round(sc, challenge.data()));
 	}
 
-	// multi-GPU sharding (this build's extension; see binius_ntt_amd.h)
+	// Multi-GPU sharding and the device-resident round exchange (this build's extensions; see
+	// binius_ntt_amd.h and INTEGRATION.md section 4). A shard prover's round messages are partial:
+	// the caller XORs them over the ranks; once needs_gather(), the ranks' exported batches are
+	// concatenated rank-major and imported by every rank, which then continues unsharded
+	// (the reference's hand-over at 32 evaluations, sumcheck.cuh:283-297).
 	void set_shard(int rank, int world) { ulvt::bn_check(bn_sumcheck_set_shard(sc, rank, world)); }
+	bool needs_gather() const {
+		int flag = 0;
+		ulvt::bn_check(bn_sumcheck_needs_gather(sc, &flag));
+		return flag != 0;
+	}
+	std::vector<uint32_t> export_shard() const {
+		std::vector<uint32_t> out((size_t)COMPOSITION_SIZE * 128);
+		ulvt::bn_check(bn_sumcheck_export_shard(sc, out.data(), out.size()));
+		return out;
+	}
+	void import_gathered(const std::vector<uint32_t>& words, int world) {
+		ulvt::bn_check(bn_sumcheck_import_gathered(sc, words.data(), words.size(), world));
+	}
+	// device sink (>= 37 words of device memory): the raw points and the flag word of every later
+	// round; round_messages_sink() queues the round on stream() without waiting for it
+	void set_message_sink(void* d_words) { ulvt::bn_check(bn_sumcheck_set_message_sink(sc, d_words)); }
+	void round_messages_sink() { ulvt::bn_check(bn_sumcheck_round_messages_sink(sc)); }
+	void* stream() const {
+		void* st = nullptr;
+		ulvt::bn_check(bn_sumcheck_stream(sc, &st));
+		return st;
+	}
 
 private:
 	bn_sumcheck* sc = nullptr;

@@ -11,6 +11,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>  // the sharded test's device message sinks (host API only)
+
 #include "finite_fields/binary_tower.hpp"
 #include "finite_fields/binary_tower_simd.hpp"
 #include "finite_fields/circuit_generator/unrolled/binary_tower_unrolled.hpp"
@@ -230,6 +232,87 @@ static void sumcheck_protocol() {
 	check(ok, what);
 }
 
+// Two shard provers of world 2 in one process, exchanging through their device message sinks (the
+// C++ form of ShardedSumcheck's device path): per round the sinks are
+// copied back on each prover's stream and XOR-ed, p(1) is completed from the global claim when the
+// flag word says it was skipped, and at the endgame the exported batches are gathered. Every round
+// must equal the unsharded prover's.
+template <uint32_t N, uint32_t D>
+static void sharded_sink_protocol() {
+	using u128 = unsigned __int128;
+	const size_t words = 4 * ((size_t)1 << N) * D;
+	std::vector<uint32_t> evals(words);
+	std::mt19937_64 g(0x5d00 + D);
+	for (auto& w : evals) w = (uint32_t)g();
+	Sumcheck<N, D, true> ref(evals, false), s0(evals, false), s1(evals, false);
+	s0.set_shard(0, 2);
+	s1.set_shard(1, 2);
+	constexpr size_t kSink = 40;
+	uint32_t* d_sink[2] = {nullptr, nullptr};
+	bool ok = hipMalloc((void**)&d_sink[0], kSink * 4) == hipSuccess && hipMalloc((void**)&d_sink[1], kSink * 4) == hipSuccess;
+	if (ok) {
+		s0.set_message_sink(d_sink[0]);
+		s1.set_message_sink(d_sink[1]);
+	}
+	auto big = [](const uint32_t* w) {
+		u128 x = 0;
+		std::memcpy(&x, w, 16);
+		return x;
+	};
+	u128 claim = 0;
+	bool gathered = false;
+	for (uint32_t round = 0; ok && round <= N; round++) {
+		std::array<uint32_t, 4> sum{}, rs{};
+		std::array<uint32_t, 4 * (D + 1)> points{}, rp{};
+		if (!gathered && s0.needs_gather()) {
+			std::vector<uint32_t> all = s0.export_shard(), e1 = s1.export_shard();
+			all.insert(all.end(), e1.begin(), e1.end());
+			s0.import_gathered(all, 2);
+			s1.import_gathered(all, 2);
+			gathered = true;
+		}
+		if (gathered) {
+			s0.this_round_messages(sum, points);
+		} else {
+			s0.round_messages_sink();
+			s1.round_messages_sink();
+			uint32_t h[2][kSink];
+			Sumcheck<N, D, true>* sp[2] = {&s0, &s1};
+			for (int k = 0; k < 2; k++)
+				ok = ok && hipMemcpyAsync(h[k], d_sink[k], sizeof h[k], hipMemcpyDeviceToHost, (hipStream_t)sp[k]->stream()) == hipSuccess &&
+				     hipStreamSynchronize((hipStream_t)sp[k]->stream()) == hipSuccess;
+			ok = ok && h[0][36] == h[1][36];
+			for (size_t i = 0; i < 4 * (D + 1); i++) points[i] = h[0][i] ^ h[1][i];
+			if (h[0][36] & 2u) {  // the last call: prod_j f_j(r)
+				std::memcpy(sum.data(), points.data(), 16);
+				points.fill(0);
+			} else if (h[0][36] & 1u) {  // p(1) left out: the global claim completes it
+				const u128 p1 = claim ^ big(points.data());
+				std::memcpy(points.data() + 4, &p1, 16);
+				std::memcpy(sum.data(), &claim, 16);
+			} else {
+				const u128 sm = big(points.data()) ^ big(points.data() + 4);
+				std::memcpy(sum.data(), &sm, 16);
+			}
+		}
+		ref.this_round_messages(rs, rp);
+		ok = ok && rs == sum && (round == N || rp == points);
+		if (round < N) {
+			std::array<uint32_t, 4> ch;
+			for (auto& w : ch) w = (uint32_t)g();
+			claim = evaluate_univariate_given_points(big(ch.data()), (const u128*)points.data(), D + 1);
+			ref.move_to_next_round(ch);
+			s0.move_to_next_round(ch);
+			if (!gathered) s1.move_to_next_round(ch);
+		}
+	}
+	for (uint32_t* p : d_sink)
+		if (p) (void)hipFree(p);
+	char what[96];
+	std::snprintf(what, sizeof(what), "Sumcheck<%u, %u, true> world-2 shards through device message sinks", N, D);
+	check(ok && gathered, what);
+}
+
 int main() {
 	check(check_gpu_capabilities(), "check_gpu_capabilities");
 	for (int log_h = 1; log_h <= 20; log_h++) ntt32_md5(log_h, 0);
@@ -244,6 +327,8 @@ int main() {
 	sumcheck_protocol<12, 3, true>();
 	sumcheck_protocol<11, 2, false>();
 	sumcheck_protocol<10, 4, true>();
+	sharded_sink_protocol<12, 3>();
+	sharded_sink_protocol<11, 2>();
 	std::printf("%d failure(s)\n", failures);
 	return failures ? 1 : 0;
 }

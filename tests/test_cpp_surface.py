@@ -20,6 +20,9 @@ BIN = os.path.join(ROOT, "tests", "cpp", "build", "test_surface")
 PRIME_BIN = os.path.join(ROOT, "tests", "cpp", "build", "test_prime_field")
 
 
+ROCM = "/opt/rocm"
+
+
 def _build(src="test_surface.cpp", out=BIN):
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-Wextra",
@@ -27,6 +30,9 @@ def _build(src="test_surface.cpp", out=BIN):
            os.path.join(ROOT, "tests", "cpp", src), "-o", out,
            "-L", LIBDIR, "-lbinius_ntt_amd", "-L", ORACLE, "-loracle",
            "-Wl,-rpath," + LIBDIR, "-Wl,-rpath," + ORACLE, "-Wl,--allow-shlib-undefined"]
+    if src == "test_surface.cpp":  # device message sinks of the sharded test (HIP host API)
+        cmd += ["-D__HIP_PLATFORM_AMD__", "-I", os.path.join(ROCM, "include"), "-L", os.path.join(ROCM, "lib"),
+                "-lamdhip64", "-Wl,-rpath," + os.path.join(ROCM, "lib")]
     subprocess.check_call(cmd)
 
 
