@@ -18,6 +18,8 @@
 //   c_lo = P00 + P11,  c_hi = P01 + P10 + alpha(P11)
 // and the quad trades halves through LDS. Operands and partial products travel through a
 // 1 KiB LDS slot per quad, so a lane never holds more than ~4 x 32 words of field data.
+// The big folds, whose second operand is the wave-uniform challenge, run on lane pairs with
+// constant-operand circuits instead (sc_fold_pair).
 //
 // Round messages are reduced without ever forming 128-word sums: after each product a lane
 // folds its 32 result words into one word of parities (bit i = XOR over the elements of bit i),
@@ -402,6 +404,89 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_coal(ScArgs A) {
 	}
 }
 
+// Big-mode fold on lane PAIRS (n_pairs % 32 == 0): the product r (lo + hi) has a constant operand,
+// the same challenge r for every lane, so its Karatsuba leaves and sums are scalar work. Lane u of
+// a pair holds the GF(2^64) half a_u (words 64u..64u+63) of s = lo + hi and forms, with r = r0 +
+// r1 X (compact words A.r[0..3]),
+//   T = a_u r1            (bsm6_fma_w2: three GF(2^32) circuits whose twiddle side is SGPR bits)
+//   the pair swaps T (DPP): lane 0 gets a_1 r1, lane 1 gets a_0 r1
+//   lane 0: a_0 r0 + a_1 r1                 = c_lo
+//   lane 1: a_1 r0 + a_0 r1 + alpha64(a_1 r1) = c_hi
+// (the schoolbook top level of quad_mul with P_ij = a_i r_j). Per product: 6 constant-operand
+// GF(2^32) circuits on 2 lanes instead of 12 general ones on 4, and no operand rows in LDS.
+// A wave takes 32 consecutive pairs of one column: coalesced 16-B loads as sc_fold_coal, staged
+// in LDS rows of 64 words padded to 68 (16 lanes of a ds_read_b128 then hit distinct banks).
+constexpr int kPairRowWords = 68;
+constexpr int kPairWaveWords = 64 * kPairRowWords;  // 64 lane rows per wave
+constexpr int kPairItemsPerWG = kScThreads / 2;
+constexpr size_t kPairMinItems = 384 * (size_t)kPairItemsPerWG;
+__device__ __forceinline__ uint32_t* pair_addr(uint32_t* slot, int w) { return slot + (w >> 6) * kPairRowWords + (w & 63); }
+
+__global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_pair(ScArgs A) {
+	extern __shared__ uint32_t lds[];
+	const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, u = lane & 1;
+	uint32_t* slot = lds + wave * kPairWaveWords;
+	const size_t it0 = (size_t)blockIdx.x * kPairItemsPerWG + 32 * wave;  // the wave's first item
+	if (it0 >= (size_t)A.d * A.n_pairs) return;
+	const int j = (int)(it0 / A.n_pairs);
+	const size_t p0 = it0 % A.n_pairs;
+	uint32_t* lo = A.cols + (size_t)j * A.col_stride + 128 * p0;
+	const uint32_t* hi = lo + 128 * A.hb;
+#pragma unroll
+	for (int i = 0; i < 16; i++) {
+		const int w = 4 * lane + 256 * i;
+		const uint4 a = *(const uint4*)(lo + w), b = *(const uint4*)(hi + w);
+		*(uint4*)pair_addr(slot, w) = make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
+	}
+	wsync();
+	uint32_t* row = slot + lane * kPairRowWords;
+	uint32_t x[64], t[64];
+#pragma unroll
+	for (int i = 0; i < 64; i += 4) {
+		const uint4 v = *(const uint4*)(row + i);
+		x[i] = v.x, x[i + 1] = v.y, x[i + 2] = v.z, x[i + 3] = v.w;
+	}
+#pragma unroll
+	for (int i = 0; i < 64; i++) t[i] = 0;
+	const uint32_t m = 0u - (uint32_t)u;
+	uint32_t o[64];
+#ifdef BN_DEV
+	if (!(A.dbg & 2))
+#endif
+	bsm6_fma_w2(x, A.r[2], A.r[3], t);  // a_u r1
+	{
+		// alpha64(T) = (T.hi, T.lo + alpha(T.hi)), kept by lane 1 only
+		uint32_t ah[32];
+		bs_alpha<5>(t + 32, ah);
+#pragma unroll
+		for (int i = 0; i < 32; i++) {
+			o[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)t[i], 0xB1, 0xF, 0xF, false) ^ (t[32 + i] & m);
+			o[32 + i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)t[32 + i], 0xB1, 0xF, 0xF, false) ^ ((t[i] ^ ah[i]) & m);
+		}
+	}
+	// x is re-read from the row (not kept live across the swap): otherwise the compiler shares
+	// the two products' data-side Karatsuba sums and keeps them all live (hundreds of spills)
+	wsync();
+#pragma unroll
+	for (int i = 0; i < 64; i += 4) {
+		const uint4 v = *(const uint4*)(row + i);
+		x[i] = v.x, x[i + 1] = v.y, x[i + 2] = v.z, x[i + 3] = v.w;
+	}
+#ifdef BN_DEV
+	if (!(A.dbg & 2))
+#endif
+	bsm6_fma_w2(x, A.r[0], A.r[1], o);  // + a_u r0
+#pragma unroll
+	for (int i = 0; i < 64; i += 4) *(uint4*)(row + i) = make_uint4(o[i], o[i + 1], o[i + 2], o[i + 3]);
+	wsync();
+#pragma unroll
+	for (int i = 0; i < 16; i++) {
+		const int w = 4 * lane + 256 * i;
+		const uint4 a = *(const uint4*)(lo + w), q = *(const uint4*)pair_addr(slot, w);
+		*(uint4*)(lo + w) = make_uint4(a.x ^ q.x, a.y ^ q.y, a.z ^ q.z, a.w ^ q.w);
+	}
+}
+
 // ---------------------------------------------------------------------------------------
 // Round server for the last rounds (at most kServerMaxCur evaluations per column left): ONE
 // resident 768-thread workgroup runs every remaining round by itself. It waits for the host's
@@ -739,9 +824,24 @@ int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 	// extra combine phase cost what its shorter circuit saved, c4 trace of round 4)
 	const int tier = (!fold && items <= wide_max) ? 2 : items <= hex_max ? 1 : 0;
 	const size_t per_wg = tier == 2 ? Grp<64>::kGroups : tier == 1 ? Grp<16>::kGroups : Grp<4>::kGroups;
-	const size_t grid = (items + per_wg - 1) / per_wg;
+	size_t grid = (items + per_wg - 1) / per_wg;
 	void* args[] = {&A};
 	const bool coal = fold && tier == 0 && A.mode == 0 && A.n_pairs % 16 == 0;
+	// (lane pairs take 128 items per workgroup, half of sc_fold_coal's grid: below ~1.5 workgroups per
+	// CU the quad fold's wider grid wins, c4 rounds 5-6: 28.0 / 24.6 vs 22.6 / 16.3 us)
+	bool pair = fold && tier == 0 && A.mode == 0 && A.n_pairs % 32 == 0 && items >= kPairMinItems;
+#ifdef BN_DEV
+	{
+		static const char* ep = getenv("BN_SC_FOLD_PAIR");
+		if (ep && atoi(ep) == 0) pair = false;
+	}
+#endif
+	if (pair) {  // lane-pair products with a scalar challenge (sc_fold_pair)
+		grid = (items + kPairItemsPerWG - 1) / kPairItemsPerWG;
+		BN_HIP(hipLaunchKernel((const void*)sc_fold_pair, dim3((unsigned)grid), dim3(kScThreads), args,
+		                       sizeof(uint32_t) * 4 * kPairWaveWords, sc->stream));
+		return BN_OK;
+	}
 	const void* fns[3][2][3] = {
 		{{(const void*)sc_messages<0, 4>, (const void*)sc_messages<1, 4>, (const void*)sc_messages<2, 4>},
 		 {coal ? (const void*)sc_fold_coal : (const void*)sc_fold<0, 4>, (const void*)sc_fold<1, 4>, (const void*)sc_fold<2, 4>}},
@@ -878,12 +978,12 @@ int sc_common_init(bn_sumcheck* sc) {
 #ifdef BN_DEV
 	if (const char* e = getenv("BN_SC_SERVER_MAX_CUR")) sc->server_max_cur = (size_t)atol(e);
 #endif
-	const void* fns[16] = {(const void*)sc_messages<0, 4>,  (const void*)sc_messages<1, 4>,  (const void*)sc_messages<2, 4>,
+	const void* fns[17] = {(const void*)sc_messages<0, 4>,  (const void*)sc_messages<1, 4>,  (const void*)sc_messages<2, 4>,
 						   (const void*)sc_fold<0, 4>,      (const void*)sc_fold<1, 4>,      (const void*)sc_fold<2, 4>,
 						   (const void*)sc_messages<0, 16>, (const void*)sc_messages<1, 16>, (const void*)sc_messages<2, 16>,
 						   (const void*)sc_fold<0, 16>,     (const void*)sc_fold<1, 16>,     (const void*)sc_fold<2, 16>,
 						   (const void*)sc_messages<0, 64>, (const void*)sc_messages<1, 64>, (const void*)sc_messages<2, 64>,
-						   (const void*)sc_fold_coal};
+						   (const void*)sc_fold_coal, (const void*)sc_fold_pair};
 	const int lds_max = (int)std::max(lds_bytes<4>(), std::max(lds_bytes<16>(), lds_bytes<64>()));
 	for (const void* f : fns) BN_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
 	return BN_OK;

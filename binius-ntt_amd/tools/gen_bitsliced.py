@@ -366,6 +366,154 @@ class LutEmitter:
                     raise AssertionError("LUT mapping differs from the DAG")
 
 
+class ScalarLutEmitter(LutEmitter):
+    """LutEmitter for circuits with a wave-uniform compact operand (gen_fma_w2): the nodes that
+    depend on that operand only (its leaves, Karatsuba sums and their XORs) are scalar work and
+    enter the 3-input cover as free inputs; the cover maps the vector network alone."""
+
+    def __init__(self, dag, roots, scalar_inputs):
+        super().__init__(dag, roots)
+        self.scalar = set()
+        for n, (op, args) in enumerate(dag.nodes):
+            if op == "in":
+                if args[0] in scalar_inputs:
+                    self.scalar.add(n)
+            elif all(a in self.scalar for a in args):
+                self.scalar.add(n)
+
+    def _cuts(self, order):
+        d = self.d
+        cuts = {}
+        for n in order:
+            op, args = d.nodes[n]
+            if op == "in" or n in self.scalar:
+                cuts[n] = [frozenset([n])]
+                continue
+            a, b = args
+            cs = set()
+            for ca in cuts[a]:
+                for cb in cuts[b]:
+                    u = ca | cb
+                    if len(u) <= self.K:
+                        cs.add(u)
+            cs = sorted(cs, key=lambda c: (len(c), sorted(c)))[: self.CUTS_PER_NODE]
+            cuts[n] = cs + [frozenset([n])]
+        return cuts
+
+    def _map(self, order, cuts, refs):
+        d = self.d
+        af = {}
+        best = {}
+        for n in order:
+            if d.nodes[n][0] == "in" or n in self.scalar:
+                af[n] = 0.0
+                continue
+            bc, bv = None, None
+            for c in cuts[n]:
+                if n in c:
+                    continue
+                v = 1.0 + sum(af[l] / max(1, refs.get(l, 1)) for l in c)
+                if bv is None or v < bv - 1e-9 or (abs(v - bv) <= 1e-9 and len(c) < len(bc)):
+                    bc, bv = c, v
+            best[n] = bc
+            af[n] = bv
+        mapped = {}
+        need = list(self.roots)
+        while need:
+            n = need.pop()
+            if n in mapped or d.nodes[n][0] == "in" or n in self.scalar:
+                continue
+            mapped[n] = best[n]
+            need.extend(best[n])
+        return mapped
+
+    def emit(self, input_map, outputs, barrier_every=0):
+        mapped = self.build()
+        d = self.d
+        # scalar nodes the cover reads, with their scalar arguments
+        sneed = set()
+        stack = [l for c in mapped.values() for l in c if l in self.scalar]
+        while stack:
+            n = stack.pop()
+            if n in sneed or d.nodes[n][0] == "in":
+                continue
+            sneed.add(n)
+            stack.extend(d.nodes[n][1])
+        name = {}
+        lines = []
+        cnt = 0
+
+        def nm(x):
+            op, args = d.nodes[x]
+            return input_map[args[0]] if op == "in" else name[x]
+        for n in sorted(set(mapped) | sneed):
+            v = "t%d" % cnt
+            cnt += 1
+            op, args = d.nodes[n]
+            if n in sneed:
+                if op.startswith("csum:"):
+                    expr = "%s ^ (%s >> %s)" % (nm(args[0]), nm(args[0]), op[5:])
+                elif op.startswith("wleaf:"):
+                    expr = "BN_BIT(%s, %s)" % (nm(args[0]), op[6:])
+                else:
+                    expr = "%s %s %s" % (nm(args[0]), "&" if op == "and" else "^", nm(args[1]))
+            else:
+                leaves = sorted(mapped[n])
+                tt = self._truth(n, leaves)
+                a = [nm(l) for l in leaves]
+                if len(leaves) == 2 and tt == 0xF0 ^ 0xCC:
+                    expr = "%s ^ %s" % tuple(a)
+                elif len(leaves) == 2 and tt == 0xF0 & 0xCC:
+                    expr = "%s & %s" % tuple(a)
+                else:
+                    while len(a) < 3:
+                        a.append(a[0])
+                    expr = "BN_BITOP3(%s, %s, %s, 0x%02x)" % (a[0], a[1], a[2], tt)
+            lines.append("const uint32_t %s = %s;" % (v, expr))
+            name[n] = v
+            if barrier_every and cnt % barrier_every == 0:
+                lines.append("BN_SCHED_BARRIER();")
+        for lv, r in outputs:
+            lines.append("%s = %s;" % (lv, "0u" if r is None else nm(r)))
+        self._selfcheck(outputs)
+        return lines
+
+    def _selfcheck(self, outputs, trials=4):
+        """As LutEmitter's, with the scalar nodes as free random inputs on both sides."""
+        import random
+        d = self.d
+        rnd = random.Random(1234)
+        for _ in range(trials):
+            ref = {}
+            for i, (op, args) in enumerate(d.nodes):
+                if op == "in" or i in self.scalar:
+                    ref[i] = rnd.getrandbits(64)
+            got = dict(ref)
+
+            def ev_ref(x):
+                if x in ref:
+                    return ref[x]
+                op, args = d.nodes[x]
+                a, b = ev_ref(args[0]), ev_ref(args[1])
+                ref[x] = (a & b) if op == "and" else (a ^ b)
+                return ref[x]
+            for n in sorted(self.mapped):
+                leaves = sorted(self.mapped[n])
+                tt = self._truth(n, leaves)
+                vals = [got[l] for l in leaves]
+                while len(vals) < 3:
+                    vals.append(vals[0])
+                a, b, c = vals
+                r = 0
+                for i in range(8):
+                    if (tt >> i) & 1:
+                        r |= (a if (i >> 2) & 1 else ~a) & (b if (i >> 1) & 1 else ~b) & (c if i & 1 else ~c)
+                got[n] = r & ((1 << 64) - 1)
+            for _, r in outputs:
+                if r is not None and got[r] != ev_ref(r):
+                    raise AssertionError("LUT mapping differs from the DAG")
+
+
 EMITTER = os.environ.get("BN_GEN_EMITTER", "auto")
 
 
@@ -384,6 +532,10 @@ def count_ops(lines):
 
 
 BARRIER_EVERY = int(os.environ.get("BN_GEN_BARRIER_EVERY", "0"))
+# gen_fma_w2: scheduling barriers keep the scalar leaf extractions next to their uses (without
+# them the scheduler hoists the SALU work and its SGPRs spill)
+W2_BARRIER_EVERY = int(os.environ.get("BN_GEN_W2_BARRIER_EVERY", "32"))
+W2_LUT = int(os.environ.get("BN_GEN_W2_LUT", "1"))
 
 
 def gen_full(h):
@@ -546,6 +698,32 @@ def gen_fma_tw(h):
     return e.emit(imap, [("out[%d]" % i, o[i]) for i in range(n)], BARRIER_EVERY)
 
 
+def gen_fma_w2():
+    """out ^= a * (w0 + w1 X) in GF(2^64): a is 64 bitsliced words, w0 and w1 are the compact
+    GF(2^32) halves of a constant that is the same for every lane of the wave (the sumcheck fold's
+    challenge, sc_fold_pair). The twiddle side (leaves, Karatsuba sums of the halves) is then
+    scalar work; the vector side is the three GF(2^32) circuits' data half only. Top level
+    accumulated eagerly as gen_fma_tw."""
+    d = DAG()
+    n, half = 64, 32
+    a = [d.inp("a%d" % i) for i in range(n)]
+    w0, w1 = d.inp("w0"), d.inp("w1")
+    o = [d.inp("o%d" % i) for i in range(n)]
+    a0, a1 = a[:half], a[half:]
+    z2 = kara_w(d, a1, w1, 0, 5)
+    az2 = mul_alpha(d, z2, 5)
+    o = [d.xor(o[i], z2[i]) for i in range(half)] + [d.xor(d.xor(o[half + i], z2[i]), az2[i]) for i in range(half)]
+    z0 = kara_w(d, a0, w0, 0, 5)
+    o = [d.xor(o[i], z0[i]) for i in range(half)] + [d.xor(o[half + i], z0[i]) for i in range(half)]
+    z1 = kara_w(d, vadd(d, a0, a1), d.xor(w0, w1), 0, 5)
+    o = o[:half] + [d.xor(o[half + i], z1[i]) for i in range(half)]
+    imap = {"a%d" % i: "a[%d]" % i for i in range(n)}
+    imap.update({"w0": "w0", "w1": "w1"})
+    imap.update({"o%d" % i: "out[%d]" % i for i in range(n)})
+    e = ScalarLutEmitter(d, o, ("w0", "w1")) if W2_LUT else Emitter(d, o)
+    return e.emit(imap, [("out[%d]" % i, o[i]) for i in range(n)], W2_BARRIER_EVERY)
+
+
 def gen_acc(h):
     """out ^= a * b (out must not alias a or b): the product's last XOR per word also takes the
     accumulator, so the register-tile butterflies (u ^= w*v) need no product array."""
@@ -629,6 +807,10 @@ def main():
             parts.append("// out ^= a * b on the %d GF(2^%d) coordinates of 32-word limbs, b shared (2^%d words): %d gates" % (cnt, 1 << h, h, count_ops(ml)))
             parts.append(fn("void bsm%dx%d_mul_acc(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint32_t* __restrict__ out)" % (h, cnt), ml))
             stats.append((h, "acc x%d" % cnt, count_ops(ml)))
+    wl = gen_fma_w2()
+    parts.append("// out ^= a * (w0 + w1 X) in GF(2^64), w0 / w1 compact and wave-uniform (scalar leaves); out must not alias a: %d gates" % count_ops(wl))
+    parts.append(fn("void bsm6_fma_w2(const uint32_t* __restrict__ a, uint32_t w0, uint32_t w1, uint32_t* __restrict__ out)", wl))
+    stats.append((6, "fma_w2", count_ops(wl)))
     parts.append("}  // namespace bn")
     with open(OUT, "w") as f:
         f.write("\n".join(parts) + "\n")
