@@ -194,6 +194,18 @@ __device__ __forceinline__ void bs_pass_body(const BsParams& P, size_t tile0) {
 #pragma unroll
 			for (int i = 0; i < 32; i += 4) *(uint4*)(U + i) = *(const uint4*)(pu + i);
 		}
+		// the stage on the top tile bit: qu's bits 0..5 are the lane's, and when none of them moves
+		// the twiddle (twt[j][0..5] = 0: the tile's other bits are lower stages) it is the
+		// workgroup-uniform part alone, so the circuit's twiddle side is scalar (bsm5_mul_w)
+		bool uni = FMAX == 32 && m == kBlkBits - 1 && ps.field[j] == 32 && !(BS_DBG(P) & 4);
+#pragma unroll
+		for (int mm = 0; mm < kBlkBits - 1; mm++) uni = uni && ps.twt[j][mm] == 0u;
+		if (uni) {
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+			__builtin_amdgcn_sched_barrier(0);
+			bsm5_mul_w(V, (uint32_t)__builtin_amdgcn_readfirstlane((int)cu_w[j]), Pr);
+			__builtin_amdgcn_sched_barrier(0);
+		} else {
 #pragma unroll
 		for (int i = 0; i < 32; i++) W[i] = (uint32_t)__builtin_amdgcn_sbfe(w, i, 1);
 		if (TR) {
@@ -211,6 +223,7 @@ __device__ __forceinline__ void bs_pass_body(const BsParams& P, size_t tile0) {
 			__builtin_amdgcn_sched_barrier(0);
 			mul_tw<FMAX>(ps.field[j], V, W, Pr);  // sub-field circuits reuse W: Pr must not alias it
 			__builtin_amdgcn_sched_barrier(0);
+		}
 		}
 		if (TR) {
 			uint32_t acc = 0;

@@ -724,6 +724,20 @@ def gen_fma_w2():
     return e.emit(imap, [("out[%d]" % i, o[i]) for i in range(n)], W2_BARRIER_EVERY)
 
 
+def gen_mul_w(h):
+    """out = a * w in GF(2^(2^h)), w compact and wave-uniform (the NTT's top block stage of a tile,
+    whose twiddle depends on no tile bit): the twiddle side is scalar work as in gen_fma_w2."""
+    d = DAG()
+    n = 1 << h
+    a = [d.inp("a%d" % i) for i in range(n)]
+    w = d.inp("w")
+    res = kara_w(d, a, w, 0, h)
+    imap = {"a%d" % i: "a[%d]" % i for i in range(n)}
+    imap["w"] = "w"
+    e = ScalarLutEmitter(d, res, ("w",))
+    return e.emit(imap, [("out[%d]" % i, res[i]) for i in range(n)], W2_BARRIER_EVERY)
+
+
 def gen_acc(h):
     """out ^= a * b (out must not alias a or b): the product's last XOR per word also takes the
     accumulator, so the register-tile butterflies (u ^= w*v) need no product array."""
@@ -807,6 +821,10 @@ def main():
             parts.append("// out ^= a * b on the %d GF(2^%d) coordinates of 32-word limbs, b shared (2^%d words): %d gates" % (cnt, 1 << h, h, count_ops(ml)))
             parts.append(fn("void bsm%dx%d_mul_acc(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint32_t* __restrict__ out)" % (h, cnt), ml))
             stats.append((h, "acc x%d" % cnt, count_ops(ml)))
+    ml = gen_mul_w(5)
+    parts.append("// out = a * w in GF(2^32), w compact and wave-uniform (scalar leaves); out must not alias a: %d gates" % count_ops(ml))
+    parts.append(fn("void bsm5_mul_w(const uint32_t* __restrict__ a, uint32_t w, uint32_t* __restrict__ out)", ml))
+    stats.append((5, "mul_w", count_ops(ml)))
     wl = gen_fma_w2()
     parts.append("// out ^= a * (w0 + w1 X) in GF(2^64), w0 / w1 compact and wave-uniform (scalar leaves); out must not alias a: %d gates" % count_ops(wl))
     parts.append(fn("void bsm6_fma_w2(const uint32_t* __restrict__ a, uint32_t w0, uint32_t w1, uint32_t* __restrict__ out)", wl))
