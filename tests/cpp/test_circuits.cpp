@@ -1,7 +1,8 @@
-// Host-side check of the generated constant-operand circuit bsm6_fma_w2 (the sumcheck fold's
-// lane-pair product, sc_fold_pair in binius-ntt_amd/csrc/sumcheck.hip): 32 bitsliced GF(2^64)
+// Host-side check of the generated constant-operand circuits: bsm6_fma_w2 (the sumcheck fold's
+// lane-pair product, sc_fold_pair in binius-ntt_amd/csrc/sumcheck.hip; 32 bitsliced GF(2^64)
 // elements a_e times a constant w = w0 + w1 X, accumulated into out, against the oracle's tower
-// product orc_mul(a_e, w, 6) (oracle/tower.c). The circuits are __host__ __device__, so the host
+// product orc_mul(a_e, w, 6), oracle/tower.c), bsm5_fma_tw and bsm5_mul_w (the NTT's per-lane and
+// scalar twiddle products). The circuits are __host__ __device__, so the host
 // build runs exactly the gate list the kernel runs. Prints "ok" or "FAIL ..." lines.
 #include <stdint.h>
 #include <stdio.h>
@@ -71,5 +72,24 @@ int main() {
 	}
 	if (!fails5) printf("ok bsm5_fma_tw 64 trials x 32 elements\n");
 	fails += fails5;
+	// the bitsliced passes' top tile stage (antt_bs.hip block_stage): out = a * w, w scalar
+	int failsw = 0;
+	for (int trial = 0; trial < 64; trial++) {
+		uint32_t a[32];
+		for (int e = 0; e < 32; e++) a[e] = (uint32_t)next(seed);
+		const uint32_t w = trial == 0 ? 0u : trial == 1 ? 1u : (uint32_t)next(seed);
+		uint32_t abs[32] = {0}, obs[32];
+		for (int i = 0; i < 32; i++)
+			for (int e = 0; e < 32; e++) abs[i] |= ((a[e] >> i) & 1u) << e;
+		bn::bsm5_mul_w(abs, w, obs);
+		for (int e = 0; e < 32; e++) {
+			uint32_t got = 0;
+			for (int i = 0; i < 32; i++) got |= ((obs[i] >> e) & 1u) << i;
+			const uint32_t want = (uint32_t)orc_mul(a[e], w, 5);
+			if (got != want && failsw++ < 4) printf("FAIL bsm5_mul_w trial %d element %d: %08x != %08x\n", trial, e, got, want);
+		}
+	}
+	if (!failsw) printf("ok bsm5_mul_w 64 trials x 32 elements\n");
+	fails += failsw;
 	return fails ? 1 : 0;
 }

@@ -109,8 +109,9 @@ CIRCUITS_BIN = os.path.join(ROOT, "tests", "cpp", "build", "test_circuits")
 
 
 def test_generated_constant_operand_circuits_match_oracle():
-    """bsm6_fma_w2 (the fold's scalar-challenge GF(2^64) product, sc_fold_pair) and bsm5_fma_tw (the
-    NTT's compact-twiddle product) run on the host against the oracle's tower product (CPU)."""
+    """bsm6_fma_w2 (the fold's scalar-challenge GF(2^64) product, sc_fold_pair), bsm5_fma_tw (the
+    NTT's per-lane compact-twiddle product) and bsm5_mul_w (its scalar-twiddle top stage) run on
+    the host against the oracle's tower product (CPU)."""
     os.makedirs(os.path.dirname(CIRCUITS_BIN), exist_ok=True)
     subprocess.check_call(["g++", "-std=c++17", "-O1", "-D__HIP_PLATFORM_AMD__", "-I", os.path.join(ROCM, "include"),
                            "-I", os.path.join(ROOT, "binius-ntt_amd", "csrc"),
@@ -118,4 +119,4 @@ def test_generated_constant_operand_circuits_match_oracle():
                            "-L", ORACLE, "-loracle", "-Wl,-rpath," + ORACLE])
     p = subprocess.run([CIRCUITS_BIN], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stdout + p.stderr
-    assert "ok bsm6_fma_w2" in p.stdout and "ok bsm5_fma_tw" in p.stdout
+    assert "ok bsm6_fma_w2" in p.stdout and "ok bsm5_fma_tw" in p.stdout and "ok bsm5_mul_w" in p.stdout
