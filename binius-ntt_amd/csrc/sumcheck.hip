@@ -415,7 +415,11 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_coal(ScArgs A) {
 // (the schoolbook top level of quad_mul with P_ij = a_i r_j). Per product: 6 constant-operand
 // GF(2^32) circuits on 2 lanes instead of 12 general ones on 4, and no operand rows in LDS.
 // A wave takes 32 consecutive pairs of one column: coalesced 16-B loads as sc_fold_coal, staged
-// in LDS rows of 64 words padded to 68 (16 lanes of a ds_read_b128 then hit distinct banks).
+// in LDS rows of 64 words padded to 68 (16 lanes of a ds_read_b128 then hit distinct banks). The
+// rows hold s until every lane has read its row, then lo (kept in registers from the loads), so
+// the result lo + r s needs no second read of lo from HBM (that re-read was a third of the
+// kernel's HBM reads); x stays in registers through both products, opaque to the compiler so the
+// two products do not share (and keep live) their data-side sums.
 constexpr int kPairRowWords = 68;
 constexpr int kPairWaveWords = 64 * kPairRowWords;  // 64 lane rows per wave
 constexpr int kPairItemsPerWG = kScThreads / 2;
@@ -432,11 +436,13 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_pair(ScArgs A) {
 	const size_t p0 = it0 % A.n_pairs;
 	uint32_t* lo = A.cols + (size_t)j * A.col_stride + 128 * p0;
 	const uint32_t* hi = lo + 128 * A.hb;
+	uint4 la[16];
 #pragma unroll
 	for (int i = 0; i < 16; i++) {
 		const int w = 4 * lane + 256 * i;
-		const uint4 a = *(const uint4*)(lo + w), b = *(const uint4*)(hi + w);
-		*(uint4*)pair_addr(slot, w) = make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
+		const uint4 b = *(const uint4*)(hi + w);
+		la[i] = *(const uint4*)(lo + w);
+		*(uint4*)pair_addr(slot, w) = make_uint4(la[i].x ^ b.x, la[i].y ^ b.y, la[i].z ^ b.z, la[i].w ^ b.w);
 	}
 	wsync();
 	uint32_t* row = slot + lane * kPairRowWords;
@@ -446,16 +452,18 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_pair(ScArgs A) {
 		const uint4 v = *(const uint4*)(row + i);
 		x[i] = v.x, x[i + 1] = v.y, x[i + 2] = v.z, x[i + 3] = v.w;
 	}
+	wsync();  // every row read: the rows take lo
+#pragma unroll
+	for (int i = 0; i < 16; i++) *(uint4*)pair_addr(slot, 4 * lane + 256 * i) = la[i];
 #pragma unroll
 	for (int i = 0; i < 64; i++) t[i] = 0;
-	const uint32_t m = 0u - (uint32_t)u;
-	uint32_t o[64];
 #ifdef BN_DEV
 	if (!(A.dbg & 2))
 #endif
 	bsm6_fma_w2(x, A.r[2], A.r[3], t);  // a_u r1
+	const uint32_t m = 0u - (uint32_t)u;
+	uint32_t o[64];
 	{
-		// alpha64(T) = (T.hi, T.lo + alpha(T.hi)), kept by lane 1 only
 		uint32_t ah[32];
 		bs_alpha<5>(t + 32, ah);
 #pragma unroll
@@ -464,29 +472,26 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_pair(ScArgs A) {
 			o[32 + i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)t[32 + i], 0xB1, 0xF, 0xF, false) ^ ((t[i] ^ ah[i]) & m);
 		}
 	}
-	// x is re-read from the row (not kept live across the swap): otherwise the compiler shares
-	// the two products' data-side Karatsuba sums and keeps them all live (hundreds of spills)
-	wsync();
+	// (x opaque: the compiler would otherwise share the two products' data-side sums)
 #pragma unroll
-	for (int i = 0; i < 64; i += 4) {
-		const uint4 v = *(const uint4*)(row + i);
-		x[i] = v.x, x[i + 1] = v.y, x[i + 2] = v.z, x[i + 3] = v.w;
-	}
+	for (int i = 0; i < 64; i++) asm volatile("" : "+v"(x[i]));
 #ifdef BN_DEV
 	if (!(A.dbg & 2))
 #endif
 	bsm6_fma_w2(x, A.r[0], A.r[1], o);  // + a_u r0
+	wsync();
 #pragma unroll
-	for (int i = 0; i < 64; i += 4) *(uint4*)(row + i) = make_uint4(o[i], o[i + 1], o[i + 2], o[i + 3]);
+	for (int i = 0; i < 64; i += 4) {
+		const uint4 v = *(const uint4*)(row + i);
+		*(uint4*)(row + i) = make_uint4(o[i] ^ v.x, o[i + 1] ^ v.y, o[i + 2] ^ v.z, o[i + 3] ^ v.w);
+	}
 	wsync();
 #pragma unroll
 	for (int i = 0; i < 16; i++) {
 		const int w = 4 * lane + 256 * i;
-		const uint4 a = *(const uint4*)(lo + w), q = *(const uint4*)pair_addr(slot, w);
-		*(uint4*)(lo + w) = make_uint4(a.x ^ q.x, a.y ^ q.y, a.z ^ q.z, a.w ^ q.w);
+		*(uint4*)(lo + w) = *(const uint4*)pair_addr(slot, w);
 	}
 }
-
 // ---------------------------------------------------------------------------------------
 // Round server for the last rounds (at most kServerMaxCur evaluations per column left): ONE
 // resident 768-thread workgroup runs every remaining round by itself. It waits for the host's
