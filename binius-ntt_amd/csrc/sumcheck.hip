@@ -763,6 +763,7 @@ struct bn_sumcheck {
 	unsigned long long* h_trace = nullptr;  // development build (BN_SC_TIMING): the server's phase stamps
 	double t_post = 0;                      // ... and the host's time of the last challenge post
 	bool read_this_round = false;
+	bool gathered = false;  // built by bn_sumcheck_import_gathered (no round server: server_eligible)
 };
 
 namespace {
@@ -871,8 +872,10 @@ double host_us() {
 
 // The round server takes over once at most server_max_cur evaluations per column are left (an
 // unsharded, eager prover without a message sink; composition_eval only folds)
+// (not for a replica built by import_gathered: the sharded driver runs one per rank in lockstep, and
+// several servers waiting in one process would block each other's queues for up to the timeout)
 bool server_eligible(const bn_sumcheck* sc) {
-	return sc->eager && sc->world == 1 && !sc->sink && sc->prepared && sc->cur >= 2 && sc->cur <= sc->server_max_cur;
+	return sc->eager && sc->world == 1 && !sc->sink && !sc->gathered && sc->prepared && sc->cur >= 2 && sc->cur <= sc->server_max_cur;
 }
 
 // a server that folds `cur` evaluations per column on `ticket` and posts those messages as `seq`
@@ -950,6 +953,10 @@ int wait_posted(bn_sumcheck* sc) {
 		const hipError_t e = hipStreamQuery(sc->stream);
 		if (e == hipSuccess) {
 			if (*posted == sc->seq) return BN_OK;
+			// the server may have timed out between the kCtlExit read above and the query (it then
+			// records ticket - 1 and ends, so the stream drains without a post): relaunch it
+			std::atomic_thread_fence(std::memory_order_acquire);
+			if (sc->server && ((volatile uint32_t*)sc->h_ctl)[kCtlExit] == sc->ticket - 1) continue;
 			BN_FAIL(BN_ERR_HIP, "round messages were not posted (sequence %u)", sc->seq);
 		}
 		if (e != hipErrorNotReady) BN_FAIL(BN_ERR_HIP, "round messages kernel: %s", hipGetErrorString(e));
@@ -1284,6 +1291,7 @@ extern "C" int bn_sumcheck_import_gathered(bn_sumcheck* sc, const uint32_t* word
 	sc->cur = (size_t)32 * world;
 	sc->rank = 0;
 	sc->world = 1;
+	sc->gathered = true;
 	sc->have_pts = sc->have_claim = sc->claim_pending = sc->pts_external = false;  // the shards' claims are partial: recompute point 1
 	sc->msgs_queued = false;
 	return BN_OK;
@@ -1291,6 +1299,9 @@ extern "C" int bn_sumcheck_import_gathered(bn_sumcheck* sc, const uint32_t* word
 
 extern "C" int bn_sumcheck_set_message_sink(bn_sumcheck* sc, void* d_words) {
 	BN_CHECK_ARG(sc, "NULL prover");
+	// a running round server posts to the host words only: switching the prover to a sink then would
+	// hand the caller words no kernel wrote
+	BN_CHECK_ARG(!sc->server || d_words == sc->sink, "the round server is running: set the sink before the last rounds");
 	sc->sink = (uint32_t*)d_words;
 	return BN_OK;
 }
@@ -1317,14 +1328,14 @@ extern "C" int bn_sumcheck_round_messages(bn_sumcheck* sc, uint32_t* sum, uint32
 		memcpy(points, sc->last_points, sizeof(uint32_t) * 4 * (sc->d + 1));
 		return BN_OK;
 	}
+	if (sc->claim_pending && sc->pts_external)  // checked before anything is queued
+		BN_FAIL(BN_ERR_INVALID, "the previous round's points went to the message sink: read this round there too");
 	if (!sc->msgs_queued) {
 		int rc = queue_messages(sc);
 		if (rc != BN_OK) return rc;
 	}
 	sc->msgs_queued = false;
 	int rc = BN_OK;
-	if (sc->claim_pending && sc->pts_external)
-		BN_FAIL(BN_ERR_INVALID, "the previous round's points went to the message sink: read this round there too");
 	if (sc->claim_pending) {  // last round's claim, computed while this round's kernel runs
 		rc = bn_sumcheck_interpolate(sc->last_pts, sc->d + 1, sc->pending_r, sc->claim);
 		if (rc != BN_OK) return rc;
@@ -1365,6 +1376,7 @@ extern "C" int bn_sumcheck_round_messages_sink(bn_sumcheck* sc) {
 	BN_CHECK_ARG(sc, "NULL prover");
 	BN_CHECK_ARG(sc->sink, "no message sink set (bn_sumcheck_set_message_sink)");
 	BN_CHECK_ARG(!(sc->world > 1 && sc->cur <= 32), "shard exhausted: gather (export_shard/import_gathered) first");
+	BN_CHECK_ARG(!sc->server, "the round server is running: read this round with bn_sumcheck_round_messages");
 	DeviceScope ds(sc->device);
 	if (!sc->prepared) {
 		const int prc = sc_prepare(sc);

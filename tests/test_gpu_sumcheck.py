@@ -344,6 +344,32 @@ def test_round_server_with_other_work_and_slow_host(n, d, pattern, dev):
     sc.close()
 
 
+def test_round_server_challenge_at_the_timeout(dev):
+    """The host posts each challenge about when the round server's bounded wait (200 us) ends, so
+    some posts land just before and some just after it times out, and some while its exit races the
+    host's poll (wait_posted must relaunch such a server, not report an unposted round).
+    Busy-waits swept over 120-320 us around the timeout; every transcript word against the oracle."""
+    import time
+
+    n, d = 12, 3
+    ev, ch = _case(n, d, 8181)
+    bs = O.bitslice128(ev)
+    want_s, want_p = O.sumcheck_run(bs, n, d, 1, ch)
+    delays = [120e-6 + 10e-6 * k for k in range(21)]
+    for rep in range(4):
+        sc = B.Sumcheck(n, d, True, bs)
+        for r in range(n + 1):
+            s, p = sc.this_round_messages()
+            assert np.array_equal(s, want_s[r]), "rep %d round %d sum" % (rep, r)
+            assert np.array_equal(p, want_p[r]), "rep %d round %d points" % (rep, r)
+            if r < n:
+                t_end = time.perf_counter() + delays[(rep * 7 + r) % len(delays)]
+                while time.perf_counter() < t_end:
+                    pass
+                sc.move_to_next_round(ch[r])
+        sc.close()
+
+
 def test_round_server_abandoned_prover(dev):
     """A prover destroyed while its round server waits for the next challenge releases it: the
     stream drains and a new prover on the same device runs a correct transcript afterwards."""
