@@ -22,7 +22,7 @@ with its status. Under torch.distributed every rank drives one GPU:
     phases);
   * c5.sumcheck: the 2^28-evaluation, d = 3 bitsliced sumcheck sharded by 32-element batch
     (b mod world == rank); every round all-gathers the (d + 2) x 16 B partial messages and XORs
-    them (RCCL has no XOR reduction); the endgame gathers the last batches (DESIGN.md section 7).
+    them (RCCL has no XOR reduction); the endgame gathers the last batches (DESIGN.md section 9).
 Rank 0 prints one JSON line. BENCH_DIST_BACKEND=gloo rehearses the multi-rank path on fewer
 GPUs (ranks then share devices round-robin; collectives run on CPU tensors).
 """
@@ -169,7 +169,7 @@ def limb0_check(d_out, log_h):
 
 PMC_FILE = os.path.join("profiles", "r06", "pmc_kernels.json")
 # the practical VALU ceiling of these kernels: independent 3-VGPR-operand v_bitop3_b32 streams issue
-# at ~0.34 per SIMD-cycle at any occupancy (binius-ntt_amd/tools/microbench4.hip, DESIGN.md 5.1)
+# at ~0.34 per SIMD-cycle at any occupancy (binius-ntt_amd/tools/microbench4.hip, DESIGN.md section 5.3)
 BITOP3_CEILING = VALU_PEAK_WAVE_INSTS * 0.34 / 0.5
 TARGET_HBM_FRAC = 0.60  # the north star's target fraction of the HBM roofline
 
@@ -467,7 +467,7 @@ def main():
                     "unit": "wave64 instructions/s", "frac": rate / VALU_PEAK_WAVE_INSTS,
                     # practical ceiling of this instruction mix: independent 3-VGPR-operand v_bitop3_b32
                     # streams issue at ~0.34 per SIMD-cycle at any occupancy (binius-ntt_amd/tools/
-                    # microbench4.hip, DESIGN.md section 5.1), not the nominal 0.5
+                    # microbench4.hip, DESIGN.md section 5.3), not the nominal 0.5
                     "bitop3_ceiling_frac": rate / BITOP3_CEILING,
                     "source": PMC_FILE + " (library SHA-256 checked)"}
         res = {

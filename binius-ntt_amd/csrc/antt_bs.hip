@@ -447,11 +447,11 @@ __global__ __launch_bounds__(64 * L, 2) void antt_bs_pass(BsParams P) {
 
 #ifdef BN_DEV
 // ------------------------------------------------------------------------------------
-// Experiment (development build only, BN_PERSIST3=1, tools/c3_persist_ab.sh): a
+// Experiment (development build only, BN_PERSIST3=1, EXPERIMENTS.md section 5.1): a
 // three-pass plan whose passes have at most two tiles per CU (one 2^20 transform: 256 tiles each)
 // as ONE launch of the variant-1 pass bodies with a grid-wide barrier between the passes instead of
 // kernel boundaries. Every work-group is resident, so the barrier cannot deadlock. Measured 0.157
-// ms against 0.0825 ms for the three launches: not used.
+// ms against 0.0825 ms for the three launches (EXPERIMENTS.md section 5.1, round 5): not used.
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned target) {
 	__syncthreads();
@@ -809,7 +809,14 @@ static std::vector<BsPass> plan_passes(const bn_antt_plan* plan) {
 		}
 		return p;
 	};
-	const int rest = log_h - kMinLogH;
+	// stages of the bottom pass: all 12 of a tile by default. BN_BOTTOM_K=11 (development build,
+	// VERDICT r5 item 5) moves its top block stage into the last upper pass (2^24: 7 + 6 + 11)
+	int bottom_k = kMinLogH;
+#ifdef BN_DEV
+	if (const char* e = getenv("BN_BOTTOM_K")) bottom_k = std::max(kMinLogH - 1, std::min(kMinLogH, atoi(e)));
+#endif
+	if (log_h - bottom_k < 1) bottom_k = kMinLogH;
+	const int rest = log_h - bottom_k;
 	const int n_up = (rest + kBlkBits - 1) / kBlkBits;
 	auto gf8_stage = [&](int s) {
 		uint32_t acc = 0;
@@ -820,22 +827,22 @@ static std::vector<BsPass> plan_passes(const bn_antt_plan* plan) {
 	int hi = log_h;
 	for (int i = 0; i < n_up; i++) {
 		const int remaining_up = n_up - i;
-		int k = (hi - kMinLogH + remaining_up - 1) / remaining_up;
+		int k = (hi - bottom_k + remaining_up - 1) / remaining_up;
 #ifndef BN_UP_EVEN
 		// the first pass takes every top stage whose twiddles lie in GF(2^8) (up to a tile's 7 bits,
 		// as long as the later passes still fit): its register-tile kernel runs near the HBM rate with
 		// VALU to spare, and each stage it takes leaves the GF(2^32) pass one stage less
 		if (i == 0 && remaining_up > 1) {
 			int g = 0;
-			while (g < kBlkBits && hi - g - 1 >= kMinLogH && gf8_stage(hi - g - 1)) g++;
-			const int min_first = (hi - kMinLogH) - (remaining_up - 1) * kBlkBits;  // the rest must still fit
+			while (g < kBlkBits && hi - g - 1 >= bottom_k && gf8_stage(hi - g - 1)) g++;
+			const int min_first = (hi - bottom_k) - (remaining_up - 1) * kBlkBits;  // the rest must still fit
 			if (g > k && g >= min_first) k = g;
 		}
 #endif
 		passes.push_back(make(hi - k, k, false));
 		hi -= k;
 	}
-	passes.push_back(make(0, kMinLogH, true));
+	passes.push_back(make(0, bottom_k, true));
 	for (size_t i = 0; i < passes.size(); i++) {
 		const bool first = i == 0, last = i + 1 == passes.size();
 		passes[i].role = first && last ? ROLE_SINGLE : first ? ROLE_FIRST : last ? ROLE_LAST : ROLE_MID;
@@ -951,8 +958,8 @@ static BsDevKnobs dev_knobs() {
 
 // GF(2^16/32) LDS-tile upper passes of fewer tiles than two per CU (one 2^20 transform) run
 // lane-split (antt_bs3_pass: two waves per product, two waves per SIMD instead of one). 2^20 A/B
-// (tools/ab_split.sh): upper GF(2^32) pass 0.0139 vs 0.0158 ms, bottom pass 0.0514 vs 0.0496 ms,
-// so the bottom pass keeps one wave per limb
+// (EXPERIMENTS.md section 5.1, round 4): upper GF(2^32) pass 0.0139 vs 0.0158 ms, bottom pass 0.0514 vs 0.0496 ms,
+// so the bottom pass keeps one wave per limb (EXPERIMENTS.md section 5.1, round 4)
 // Development build only (BN_MID_PF=1): GF(2^16/32) middle passes on antt_rr_mid_pf, the
 // register-tile kernel that hides the next tile's loads. Measured slower than antt_bs_pass at 2^24
 // (pass 1 0.224-0.229 vs 0.189-0.193 ms), so the product never selects it.
@@ -978,7 +985,7 @@ static bool use_split(const bn_antt_plan* plan, const BsPass& pass, size_t ntile
 
 // Bottom pass of a small launch (fewer tiles than two per CU: one wave per SIMD either way) on
 // register tiles, compiled without the three-waves bound (antt_rr.hip small_last): C3 (one 2^20
-// transform) 0.0800-0.0802 vs 0.0822-0.0824 ms on LDS tiles (round 5, tools/r05_c3_rrlast.sh).
+// transform) 0.0800-0.0802 vs 0.0822-0.0824 ms on LDS tiles (round 5, EXPERIMENTS.md section 5.1).
 // BN_RR_LAST=0 (development build) keeps it on LDS tiles.
 static bool use_rr_last(const bn_antt_plan* plan, const BsPass& pass, size_t ntiles, const BsDevKnobs& kn) {
 	if (kn.rr_last == 0 || plan->variant != 5 || plan->limbs != 4 || pass.role != ROLE_LAST) return false;

@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void k_bitslice(uint32_t* buf, size_t nblk, in
 // the quad's LDS slot and stores limb l of the product), so no lane holds more than ~4 x 32 words.
 // One block per quad and no loop: a persistent grid that prefetched the next block's operands
 // kept them live across the product, and the spills (432 B/lane) made it 1.9x slower (3.4e10 vs
-// 6.2-6.5e10 products/s, DESIGN.md section 5.4). Every operand word is read into the slot before any
+// 6.2-6.5e10 products/s, DESIGN.md section 7). Every operand word is read into the slot before any
 // output word is written: alias-safe for o == a or o == b (core.cu:21).
 __global__ __launch_bounds__(256, 2) void k_gf128_mul_bs(const uint32_t* a, const uint32_t* b, uint32_t* o, size_t nblk) {
 	extern __shared__ uint32_t lds[];

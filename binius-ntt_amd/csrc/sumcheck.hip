@@ -41,7 +41,10 @@
 namespace bn {
 namespace {
 
-constexpr int kScThreads = 256;  // (512-thread workgroups, one per CU: 6 % slower on c4)
+#ifndef BN_SC_THREADS
+#define BN_SC_THREADS 256
+#endif
+constexpr int kScThreads = BN_SC_THREADS;  // (512-thread workgroups, one per CU: 6 % slower on c4)
 constexpr int kScMinWG = 512 / kScThreads;  // 2 waves per SIMD (256 VGPRs)
 constexpr int kQuadsPerWG = kScThreads / 4;
 // Round messages are XOR-accumulated into kAccCopies copies of the (kMaxD + 1) x 4-word point
@@ -182,7 +185,7 @@ __device__ __forceinline__ void post_points(const ScArgs& A, int t) {
 
 // Timing-experiment builds only (make BUILD=build-x LIBDIR=lib-x EXTRA=-DBN_SC_SKIP_MID): the
 // big rounds' quad products run 8 of their 12 GF(2^32) circuits (wrong results), the upper bound
-// on what a 9-circuit Karatsuba top level could save.
+// on what a 9-circuit Karatsuba top level could save (EXPERIMENTS.md section 5.3, round 5).
 #ifdef BN_SC_SKIP_MID
 constexpr bool kSkipMid = true;
 #else

@@ -398,7 +398,7 @@ def test_big_rounds_host_patterns(n, d, pattern, dev):
     prover's stream between rounds ("busy"), rounds whose messages are never read ("skip": the next
     round then computes p(1) from the data) and rounds read twice ("reread"). The transcript must be
     the oracle's word for word. (Round 5 ran these against pre-enqueued folds that wait on the GPU
-    for their challenge; that design was measured slower and removed, DESIGN.md section 5.3.)"""
+    for their challenge; that design was measured slower and removed, DESIGN.md section 6.)"""
     import time
 
     import torch

@@ -1,13 +1,12 @@
 #!/bin/bash
-# Round-5 evidence beside tools/final_evidence.sh, into gpurun_out/profile_r05/:
+# Evidence beside tools/final_evidence.sh, into gpurun_out/profile_$ROUND_DIR/ (default r06):
 #   sumcheck c4 d=3: rocprofv3 kernel trace + stats, per-round timeline, PMC (SQ and stall groups);
-#   C3 (one 2^20 transform): kernel traces of the default three launches and of the persistent
-#   single-launch experiment (dev build, BN_PERSIST3=1, variant 1).
+#   C3 (one 2^20 transform): kernel trace + stats of its three launches.
 # Each GPU step has its own time limit; the first failure ends the script.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"
-P="$R/gpurun_out/profile_r05"
+P="$R/gpurun_out/profile_${ROUND_DIR:-r06}"
 mkdir -p "$P"
 export TMPDIR=/tmp
 bash tools/prof_sumcheck.sh > /dev/null || exit 1
@@ -23,5 +22,5 @@ c3() {  # tag, env...
   cp "gpurun_out/c3_$tag/run_kernel_stats.csv" "$P/c3_${tag}_kernel_stats.csv"
   grep -h '"c3"' "gpurun_out/c3_$tag.log" > "$P/c3_${tag}.json"
 }
-c3 default BN_NOTHING=1 && c3 persist3 BINIUS_NTT_AMD_LIB="$R/binius-ntt_amd/lib-dev/libbinius_ntt_amd.so" BN_ANTT_VARIANT=1 BN_PERSIST3=1 || exit 1
-echo "r05_extra done"
+c3 default BN_NOTHING=1 || exit 1
+echo "extra_evidence done"

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round evidence for profiles/rNN (default r05) on one box, for the library as built in this tree:
+# Round evidence for profiles/rNN (default r06) on one box, for the library as built in this tree:
 #   1. PMC passes (FETCH_SIZE, WRITE_SIZE, SQ) of the headline bench and of the config-2 loops, each
 #      counter group in its own rocprofv3 run (MI355X_MICROARCH.md), summarised per kernel name and
 #      stamped with the library's SHA-256 -> profiles/$R/pmc_kernels.json (read by bench.py)
@@ -7,7 +7,7 @@
 # Every GPU step has its own time limit; the first failure ends the script.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-RN=${ROUND_DIR:-r05}
+RN=${ROUND_DIR:-r06}
 cd "$R"
 mkdir -p gpurun_out "profiles/$RN"
 PMC_GROUPS=fetch,write,sq,stall PMC_TAG=hl_ PMC_ARGS="--no-cpu --no-configs --no-c5 --steps 3 --warmup 1" bash tools/pmc.sh || exit 1
