@@ -110,7 +110,7 @@ struct ScArgs {
 	size_t col_stride;  // words between columns
 	int d;
 	size_t n_pairs;     // batch pairs (big mode) or 1 (small modes)
-	size_t hb;          // batch distance of a pair (big mode)
+	size_t hb;          // batch distance of a fold pair (big mode: n_pairs, or 2 n_pairs in sc_fold_msgs)
 	int h;              // element distance of a pair inside the batch (small modes)
 	int mode;           // 0 big, 1 in-batch pairs, 2 single element (cur == 1)
 	int kmax;           // points 0..kmax
@@ -123,6 +123,8 @@ struct ScArgs {
 	uint32_t seq;       // this launch's sequence number
 	int post;           // 1: the last workgroup posts the points (small grids), 0: sc_post does
 	uint32_t kcol[kMaxD + 1][4];  // GF(2^4) products k * 2^a (interpolation point k)
+	int fm_p;                     // sc_fold_msgs: pairs per work-group P
+	uint32_t fm_magic;            // ... ceil(2^32 / (2 P)): item / (2 P) = umulhi(item, fm_magic) for items < 2^16
 	int dbg;  // development build (BN_DEV) only: BN_SC_DBG bit 0 = synthetic operands instead of
 	          // column loads, bit 1 = no products, bit 2 = no k-multiples, bit 3 = no parity
 	          // reduction (wrong results; for timing experiments)
@@ -145,7 +147,7 @@ __device__ __forceinline__ void load_pair(const ScArgs& A, int j, size_t p, int 
 #endif
 	if constexpr (MODE == 0) {
 		ld32(lo, c + 128 * p + 32 * l);
-		ld32(hi, c + 128 * (p + A.hb) + 32 * l);
+		ld32(hi, c + 128 * (p + A.n_pairs) + 32 * l);  // pairs (p, p + n_pairs): the high half
 		emask = ~0u;
 	} else if constexpr (MODE == 1) {
 		const uint32_t m = (1u << A.h) - 1u;
@@ -212,26 +214,43 @@ __device__ __forceinline__ void grp_mul(const Slot& S, const uint32_t* B, int l,
 		wide_mul<B_SHARED>(S, B, l);
 }
 
+// the work-group's point sums in LDS (after the product slots); the accumulator set of the next
+// round is cleared by workgroup 0 (rounds alternate between two sets; the other set was last read
+// back by the previous round's post, ordered before this launch, so no memset is queued per round)
+template <int G>
+__device__ __forceinline__ uint32_t* messages_init(const ScArgs& A, uint32_t* lds) {
+	uint32_t* accL = lds + Grp<G>::kSlotsWords + 128;  // (kMaxD + 1) x 4 words
+	if (threadIdx.x < 4 * (kMaxD + 1)) accL[threadIdx.x] = 0;
+	if (blockIdx.x == 0)
+		for (int i = threadIdx.x; i < kAccSet; i += kScThreads) A.clr[i] = 0;
+	return accL;
+}
+
+// point k of pair p on this group (when `valid`), then the work-group's reduction and posting
+template <int MODE, int G>
+__device__ __forceinline__ void messages_run(const ScArgs& A, uint32_t* lds, uint32_t* accL, size_t p, int k, bool valid);
+
 // One (pair, point k) per group, k fastest: the kmax+1 groups of a pair run side by side, so the
 // pair's columns are read from HBM once and hit in cache for the other points.
 template <int MODE, int G>
 __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_messages(ScArgs A) {
 	extern __shared__ uint32_t lds[];
-	const int l = threadIdx.x % G, qw = threadIdx.x / G;
-	const Slot S{lds + qw * Grp<G>::kSlotWords};
-	uint32_t* accL = lds + Grp<G>::kSlotsWords + 128;  // (kMaxD + 1) x 4 words
-	if (threadIdx.x < 4 * (kMaxD + 1)) accL[threadIdx.x] = 0;
-	// rounds alternate between two accumulator sets; the other set was last read back by the
-	// previous round's copy (ordered before this launch), so no memset is queued per round
-	if (blockIdx.x == 0)
-		for (int i = threadIdx.x; i < kAccSet; i += kScThreads) A.clr[i] = 0;
+	const int qw = threadIdx.x / G;
+	uint32_t* accL = messages_init<G>(A, lds);
 	__syncthreads();
 	const int npts = A.kmax + 1 - A.skip1;
 	const size_t item = (size_t)blockIdx.x * Grp<G>::kGroups + qw;
 	const size_t p = item / npts;
 	const int ki = (int)(item % npts);
 	const int k = (A.skip1 && ki >= 1) ? ki + 1 : ki;
-	if (p < A.n_pairs) {
+	messages_run<MODE, G>(A, lds, accL, p, k, p < A.n_pairs);
+}
+
+template <int MODE, int G>
+__device__ __forceinline__ void messages_run(const ScArgs& A, uint32_t* lds, uint32_t* accL, size_t p, int k, bool valid) {
+	const int l = threadIdx.x % G, qw = threadIdx.x / G;
+	const Slot S{lds + qw * Grp<G>::kSlotWords};
+	if (valid) {
 		uint32_t emask = 0;
 		for (int j = 0; j < A.d; j++) {
 			// f_j at point k: lo + k (lo + hi), written into the A (j == 0) or B operand
@@ -429,22 +448,23 @@ constexpr int kPairItemsPerWG = kScThreads / 2;
 constexpr size_t kPairMinItems = 384 * (size_t)kPairItemsPerWG;
 __device__ __forceinline__ uint32_t* pair_addr(uint32_t* slot, int w) { return slot + (w >> 6) * kPairRowWords + (w & 63); }
 
-__global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_pair(ScArgs A) {
-	extern __shared__ uint32_t lds[];
-	const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, u = lane & 1;
-	uint32_t* slot = lds + wave * kPairWaveWords;
-	const size_t it0 = (size_t)blockIdx.x * kPairItemsPerWG + 32 * wave;  // the wave's first item
-	if (it0 >= (size_t)A.d * A.n_pairs) return;
-	const int j = (int)(it0 / A.n_pairs);
-	const size_t p0 = it0 % A.n_pairs;
-	uint32_t* lo = A.cols + (size_t)j * A.col_stride + 128 * p0;
-	const uint32_t* hi = lo + 128 * A.hb;
+// One wave's 32 lane-pair folds. Item q < 32 of the wave folds batch lo_of(q) (nullptr: no item)
+// with the batch A.hb further on, in place. Lane t of the wave moves 16 B of item (t >> 5) + 2 i at
+// word (4 t) & 127 for i < 16: coalesced 512-B pieces.
+template <class LoOf>
+__device__ __forceinline__ void fold_pair_wave(const ScArgs& A, uint32_t* slot, int lane, LoOf lo_of) {
+	const int u = lane & 1;
 	uint4 la[16];
 #pragma unroll
 	for (int i = 0; i < 16; i++) {
 		const int w = 4 * lane + 256 * i;
-		const uint4 b = *(const uint4*)(hi + w);
-		la[i] = *(const uint4*)(lo + w);
+		const uint32_t* lo = lo_of(w >> 7);
+		uint4 b = make_uint4(0, 0, 0, 0);
+		la[i] = b;
+		if (lo) {
+			b = *(const uint4*)(lo + 128 * A.hb + (w & 127));
+			la[i] = *(const uint4*)(lo + (w & 127));
+		}
 		*(uint4*)pair_addr(slot, w) = make_uint4(la[i].x ^ b.x, la[i].y ^ b.y, la[i].z ^ b.z, la[i].w ^ b.w);
 	}
 	wsync();
@@ -492,8 +512,57 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_pair(ScArgs A) {
 #pragma unroll
 	for (int i = 0; i < 16; i++) {
 		const int w = 4 * lane + 256 * i;
-		*(uint4*)(lo + w) = *(const uint4*)pair_addr(slot, w);
+		uint32_t* lo = lo_of(w >> 7);
+		if (lo) *(uint4*)(lo + (w & 127)) = *(const uint4*)pair_addr(slot, w);
 	}
+}
+
+__global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_pair(ScArgs A) {
+	extern __shared__ uint32_t lds[];
+	const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+	const size_t it0 = (size_t)blockIdx.x * kPairItemsPerWG + 32 * wave;  // the wave's first item
+	if (it0 >= (size_t)A.d * A.n_pairs) return;
+	const int j = (int)(it0 / A.n_pairs);
+	const size_t p0 = it0 % A.n_pairs;
+	uint32_t* lo = A.cols + (size_t)j * A.col_stride + 128 * p0;
+	fold_pair_wave(A, lds + wave * kPairWaveWords, lane, [&](int q) -> uint32_t* { return lo + 128 * q; });
+}
+
+// Round i's fold fused with round i + 1's messages (the QM31 sibling's
+// qm_fold_messages in GF(2^128) form). A work-group owns P = kGroups / npts consecutive pairs
+// p0 .. p0 + P - 1 of the folded columns (pair distance hb' = A.n_pairs). Phase 1 folds the 2 P d
+// batches they consist of, p' and p' + hb' of every column (old pairs (b, b + 2 hb'), A.hb =
+// 2 hb'), on lane pairs exactly as sc_fold_pair, and writes them in place. Phase 2 runs the
+// messages of those P pairs on the quads as sc_messages, reading the batches the work-group has
+// just written (L2) instead of a second kernel reading them back from HBM; one launch per round
+// instead of two. No other work-group reads what this one writes: pair p' reads old batches p',
+// p' + hb', p' + 2 hb', p' + 3 hb' and writes p', p' + hb' only.
+__global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_msgs(ScArgs A) {
+	extern __shared__ uint32_t lds[];
+	const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+	const int npts = A.kmax + 1 - A.skip1;
+	const int P = A.fm_p;
+	const size_t p0 = (size_t)blockIdx.x * P;
+	const size_t hbn = A.n_pairs;
+	uint32_t* accL = messages_init<4>(A, lds);
+	// phase 1: item v of column j (v < 2 P) folds batch p0 + v (v < P) or hb' + p0 + v - P
+	const int items = 2 * P * A.d;
+	if (32 * wave < items) {
+		fold_pair_wave(A, lds + wave * kPairWaveWords, lane, [&](int q) -> uint32_t* {
+			const int it = 32 * wave + q;
+			if (it >= items) return nullptr;
+			const int j = (int)__umulhi((uint32_t)it, A.fm_magic), v = it - j * 2 * P;
+			const size_t pp = p0 + (size_t)(v < P ? v : v - P);
+			if (pp >= hbn) return nullptr;
+			return A.cols + (size_t)j * A.col_stride + 128 * (v < P ? pp : pp + hbn);
+		});
+	}
+	// every fold of the work-group is in memory (L2) and the fold's LDS rows are free
+	__syncthreads();
+	const int qw = threadIdx.x / 4;
+	const int lp = qw / npts, ki = qw - lp * npts;
+	const int k = (A.skip1 && ki >= 1) ? ki + 1 : ki;
+	messages_run<0, 4>(A, lds, accL, p0 + (size_t)lp, k, lp < P && p0 + (size_t)lp < hbn);
 }
 // ---------------------------------------------------------------------------------------
 // Round server for the last rounds (at most kServerMaxCur evaluations per column left): ONE
@@ -862,6 +931,61 @@ int sc_launch(bn_sumcheck* sc, bool fold, const uint32_t* r) {
 	const size_t lds = tier == 2 ? lds_bytes<64>() : tier == 1 ? lds_bytes<16>() : lds_bytes<4>();
 	BN_HIP(hipLaunchKernel(fns[tier][fold ? 1 : 0][A.mode], dim3((unsigned)grid), dim3(kScThreads), args, lds, sc->stream));
 	if (!fold && !A.post) BN_HIP(hipLaunchKernel((const void*)sc_post, dim3(1), dim3(64), args, 0, sc->stream));
+	return BN_OK;
+}
+
+// Round i's fold with r fused into round i + 1's messages (sc_fold_msgs): the big rounds whose
+// messages run on quads. Called after move_to_next_round has halved cur and updated the claim state.
+// Measured slower than separate fold + messages launches on c4 (d = 3: 3.59-3.67 vs 3.40-3.44 ms,
+// DESIGN.md section 10): the batches a work-group folds leave L2 before its messages phase reads
+// them, so the product keeps the two launches; -DBN_SC_FUSED builds the fused path (experiments).
+#ifdef BN_SC_FUSED
+constexpr bool kFusedFold = true;
+#else
+constexpr bool kFusedFold = false;
+#endif
+bool fused_eligible(const bn_sumcheck* sc) {
+	if (!kFusedFold || !sc->eager || sc->cur < 64 || (sc->world > 1 && sc->cur <= 32)) return false;
+	const int npts = sc->d + 1 - ((sc->have_claim || sc->claim_pending) ? 1 : 0);
+	return (sc->cur / 64) * (size_t)npts > kHexMaxItems && npts <= Grp<4>::kGroups;
+}
+
+int launch_fused(bn_sumcheck* sc, const uint32_t* r) {
+	ScArgs A{};
+	A.cols = sc->cols;
+	A.col_stride = sc->col_words;
+	A.d = sc->d;
+	A.mode = 0;
+	A.n_pairs = sc->cur / 64;  // pairs of the folded columns
+	A.hb = 2 * A.n_pairs;      // the fold's pair distance
+	A.kmax = sc->d;
+	A.skip1 = (sc->have_claim || sc->claim_pending) ? 1 : 0;
+	A.res = sc->d_res;
+	A.sink = sc->sink;
+	A.seq = ++sc->seq;
+	A.acc = sc->acc + kAccSet * sc->par;
+	A.clr = sc->acc + kAccSet * (1 - sc->par);
+	memcpy(A.r, r, 16);
+#ifdef BN_DEV
+	{
+		static const int dbg = getenv("BN_SC_DBG") ? atoi(getenv("BN_SC_DBG")) : 0;
+		A.dbg = dbg;
+	}
+#endif
+	for (int k = 0; k <= kMaxD; k++)
+		for (int a = 0; a < 4; a++) A.kcol[k][a] = (uint32_t)tw_mul((uint64_t)k, 1ull << a, 2);
+	const int npts = A.kmax + 1 - A.skip1;
+	const size_t P = Grp<4>::kGroups / npts;
+	A.fm_p = (int)P;
+	A.fm_magic = (uint32_t)(((1ull << 32) + 2 * P - 1) / (2 * P));
+	const size_t grid = (A.n_pairs + P - 1) / P;
+	A.post = grid <= kPostInKernelMaxWG;
+	void* args[] = {&A};
+	const size_t lds = std::max(lds_bytes<4>(), sizeof(uint32_t) * 4 * kPairWaveWords);
+	BN_HIP(hipLaunchKernel((const void*)sc_fold_msgs, dim3((unsigned)grid), dim3(kScThreads), args, lds, sc->stream));
+	if (!A.post) BN_HIP(hipLaunchKernel((const void*)sc_post, dim3(1), dim3(64), args, 0, sc->stream));
+	sc->par ^= 1;
+	sc->msgs_queued = true;
 	return BN_OK;
 }
 
@@ -1410,16 +1534,26 @@ extern "C" int bn_sumcheck_move_to_next_round(bn_sumcheck* sc, const uint32_t* c
 		if (prc != BN_OK) return prc;
 	}
 	const bool to_server = sc->server || server_eligible(sc);
-	if (!to_server) {
-		int rc = sc_launch(sc, true, challenge);
-		if (rc != BN_OK) return rc;
-	}
 	// no sync: the fold is ordered before the next round's messages on the prover's stream
 	sc->have_claim = false;  // a claim not consumed by this round's messages is stale now
 	sc->claim_pending = sc->have_pts && sc->derive_p1;
+	sc->cur /= 2;
+	const bool fused = !to_server && fused_eligible(sc);  // decided on the folded size
+	sc->cur *= 2;
+	if (!to_server && !fused) {  // (a fold launch does not read the claim state)
+		int rc = sc_launch(sc, true, challenge);
+		if (rc != BN_OK) return rc;
+	}
 	if (sc->claim_pending) memcpy(sc->pending_r, challenge, 16);
 	sc->have_pts = false;
 	sc->read_this_round = false;
+	if (fused) {
+		sc->cur /= 2;
+		sc->round++;
+		sc->sharded_used = true;
+		sc->msgs_queued = false;  // a queued, unread messages kernel ran before the fold: dropped
+		return launch_fused(sc, challenge);
+	}
 	if (to_server) {
 		// the round server folds and computes the next round's messages (p(1) skipped when the
 		// claim is derived; never for the final evaluation, which the server decides itself)

@@ -33,3 +33,33 @@ def test_bench_dry_run_relaunch_world2():
     d = _run(["--gpus", "2", "--dry-run"])
     assert d["dry_run"] and d["n_gpus"] == 2
     assert d["rank_checks"] == {"xor_exchange_ok": True, "max_over_ranks": 1.0, "batch_slices_cover": True}
+
+
+def test_valu_transform_budget(monkeypatch):
+    """bench.py's transform-level VALU roofline (VERDICT r5 item 4): the sum of the passes'
+    committed VALU counts per transform time against both ceilings, and the instruction budget the
+    north star's 60 %-of-HBM target implies at the bitop3 ceiling."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    counts = {"k0": 73.6e6, "k1": 85.9e6, "k2": 263.2e6}
+    monkeypatch.setattr(bench, "kernel_counters", lambda name: ({"SQ_INSTS_VALU": counts[name]}, None))
+
+    class Ntt:
+        def pass_kernel_name(self, i):
+            return "k%d" % i
+
+    alg = 2 * 16 * (1 << 24)
+    v = bench.valu_transform(Ntt(), 3, 0.70, alg)
+    assert v["insts_per_transform"] == sum(counts.values())
+    assert abs(v["achieved"] - 422.7e6 / 0.70e-3) < 1e3
+    # at the bitop3 ceiling (0.34 of 0.5 per SIMD-cycle) 422.7M instructions take ~0.506 ms
+    assert abs(v["floor_ms_at_ceiling"] - 0.5056) < 1e-3
+    # the 60 % target: 537 MB in 0.1118 ms -> ~93.5M instructions, 4.5x fewer than now
+    assert abs(v["target"]["ms"] - 0.11185) < 1e-4
+    assert abs(v["target"]["insts_budget_at_ceiling"] / 1e6 - 93.5) < 0.5
+    assert 4.4 < v["target"]["reduction_needed"] < 4.6
+    assert 0.13 < v["hbm_frac_cap_at_ceiling"] < 0.14
+    monkeypatch.setattr(bench, "kernel_counters", lambda name: (None, "profiled on another build"))
+    v = bench.valu_transform(Ntt(), 3, 0.70, alg)
+    assert v["insts_per_transform"] is None and "another build" in v["note"]

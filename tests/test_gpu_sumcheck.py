@@ -62,6 +62,25 @@ def test_sumcheck_transcript_quad_path(dev):
     sc.close()
 
 
+@pytest.mark.parametrize("n,d,full_points", [(19, 3, False), (19, 2, False), (19, 2, True)])
+def test_sumcheck_transcript_fused_fold_messages(n, d, full_points, dev, monkeypatch):
+    # N = 19 transcripts against the oracle, every round's sum and points. Round 1 (2^18
+    # evaluations per column left, with and without the claim-derived point 1) is the first round
+    # whose fold the -DBN_SC_FUSED experiment build runs inside the messages launch (sc_fold_msgs;
+    # this test was green on that build too).
+    if full_points:
+        monkeypatch.setenv("BN_SUMCHECK_FULL_POINTS", "1")
+    ev, ch = _case(n, d, 1900 + 10 * d + full_points)
+    bs = O.bitslice128(ev)
+    want_s, want_p = O.sumcheck_run(bs, n, d, 1, ch)
+    sc = B.Sumcheck(n, d, True, bs)
+    got_s, got_p = _transcript(sc, n, ch)
+    sc.close()
+    for r in range(n + 1):
+        assert np.array_equal(got_s[r], want_s[r]), "round %d sum" % r
+        assert np.array_equal(got_p[r], want_p[r]), "round %d points" % r
+
+
 @pytest.mark.parametrize("full_points", [False, True])
 @pytest.mark.parametrize("n,d", [(16, 3), (14, 4), (15, 2)])
 def test_sumcheck_protocol_checks(n, d, full_points, dev, monkeypatch):
