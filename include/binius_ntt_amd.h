@@ -215,7 +215,9 @@ int bn_sumcheck_needs_gather(const bn_sumcheck* sc, int* flag);
  * sum = p(0) + p(1)); bit 1 set for the last call (one evaluation left: words 0-3 are the sum,
  * prod_j f_j(r), and there are no points). The words are written before the posted sequence number, so they are complete
  * once bn_sumcheck_round_messages has returned; consumers on other streams order themselves after
- * the prover's stream (bn_sumcheck_stream) to read them. */
+ * the prover's stream (bn_sumcheck_stream) to read them. A prover with a sink never starts the
+ * resident round server; while a server started earlier runs (an unsharded prover's last rounds),
+ * setting a sink returns BN_ERR_INVALID. */
 int bn_sumcheck_set_message_sink(bn_sumcheck* sc, void* d_words);
 /* Sharded drivers with a message sink: replaces bn_sumcheck_round_messages without waiting for the
  * round. Makes sure the round's messages kernel is queued on the prover's stream and returns; the
@@ -223,7 +225,7 @@ int bn_sumcheck_set_message_sink(bn_sumcheck* sc, void* d_words);
  * bn_sumcheck_stream (e.g. enqueues its collective there) and never polls the host. The caller
  * then holds the round's global points: the next round skips p(1) when the prover derives it
  * (sink word 36 bit 0) and the caller completes it from the global claim. Once used, the rounds
- * up to the endgame gather must all be read this way. */
+ * up to the endgame gather must all be read this way. BN_ERR_INVALID while a round server runs. */
 int bn_sumcheck_round_messages_sink(bn_sumcheck* sc);
 int bn_sumcheck_stream(const bn_sumcheck* sc, void** stream);
 int bn_sumcheck_export_shard(const bn_sumcheck* sc, uint32_t* out, size_t out_words);
