@@ -52,3 +52,12 @@ def test_null_arguments_rejected():
     assert L.bn_antt_plan_destroy(None) == B.BN_OK
     assert L.bn_sumcheck_destroy(None) == B.BN_OK
     assert L.bn_gf128_mul_device(None, None, None, 4, None) == B.BN_ERR_INVALID
+
+
+def test_product_library_has_no_experiment_kernels():
+    """Experiments measured and not kept live only in the development / experiment builds (BN_DEV,
+    -DBN_SC_FUSED): the product library the driver loads carries none of their kernels."""
+    with open(B.LIB_PATH, "rb") as f:
+        blob = f.read()
+    for name in (b"antt_bs_persist3", b"antt_rr_mid_pf", b"antt_rr_pass_persist", b"sc_fold_msgs"):
+        assert name not in blob, name
