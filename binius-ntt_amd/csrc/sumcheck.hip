@@ -110,7 +110,7 @@ struct ScArgs {
 	size_t col_stride;  // words between columns
 	int d;
 	size_t n_pairs;     // batch pairs (big mode) or 1 (small modes)
-	size_t hb;          // batch distance of a fold pair (big mode: n_pairs, or 2 n_pairs in sc_fold_msgs)
+	size_t hb;          // batch distance of a pair (big mode)
 	int h;              // element distance of a pair inside the batch (small modes)
 	int mode;           // 0 big, 1 in-batch pairs, 2 single element (cur == 1)
 	int kmax;           // points 0..kmax
@@ -123,8 +123,10 @@ struct ScArgs {
 	uint32_t seq;       // this launch's sequence number
 	int post;           // 1: the last workgroup posts the points (small grids), 0: sc_post does
 	uint32_t kcol[kMaxD + 1][4];  // GF(2^4) products k * 2^a (interpolation point k)
+#ifdef BN_SC_FUSED
 	int fm_p;                     // sc_fold_msgs: pairs per work-group P
 	uint32_t fm_magic;            // ... ceil(2^32 / (2 P)): item / (2 P) = umulhi(item, fm_magic) for items < 2^16
+#endif
 	int dbg;  // development build (BN_DEV) only: BN_SC_DBG bit 0 = synthetic operands instead of
 	          // column loads, bit 1 = no products, bit 2 = no k-multiples, bit 3 = no parity
 	          // reduction (wrong results; for timing experiments)
@@ -147,7 +149,7 @@ __device__ __forceinline__ void load_pair(const ScArgs& A, int j, size_t p, int 
 #endif
 	if constexpr (MODE == 0) {
 		ld32(lo, c + 128 * p + 32 * l);
-		ld32(hi, c + 128 * (p + A.n_pairs) + 32 * l);  // pairs (p, p + n_pairs): the high half
+		ld32(hi, c + 128 * (p + A.hb) + 32 * l);
 		emask = ~0u;
 	} else if constexpr (MODE == 1) {
 		const uint32_t m = (1u << A.h) - 1u;
@@ -214,6 +216,123 @@ __device__ __forceinline__ void grp_mul(const Slot& S, const uint32_t* B, int l,
 		wide_mul<B_SHARED>(S, B, l);
 }
 
+// One (pair, point k) per group, k fastest: the kmax+1 groups of a pair run side by side, so the
+// pair's columns are read from HBM once and hit in cache for the other points.
+template <int MODE, int G>
+__global__ __launch_bounds__(kScThreads, kScMinWG) void sc_messages(ScArgs A) {
+	extern __shared__ uint32_t lds[];
+	const int l = threadIdx.x % G, qw = threadIdx.x / G;
+	const Slot S{lds + qw * Grp<G>::kSlotWords};
+	uint32_t* accL = lds + Grp<G>::kSlotsWords + 128;  // (kMaxD + 1) x 4 words
+	if (threadIdx.x < 4 * (kMaxD + 1)) accL[threadIdx.x] = 0;
+	// rounds alternate between two accumulator sets; the other set was last read back by the
+	// previous round's copy (ordered before this launch), so no memset is queued per round
+	if (blockIdx.x == 0)
+		for (int i = threadIdx.x; i < kAccSet; i += kScThreads) A.clr[i] = 0;
+	__syncthreads();
+	const int npts = A.kmax + 1 - A.skip1;
+	const size_t item = (size_t)blockIdx.x * Grp<G>::kGroups + qw;
+	const size_t p = item / npts;
+	const int ki = (int)(item % npts);
+	const int k = (A.skip1 && ki >= 1) ? ki + 1 : ki;
+	if (p < A.n_pairs) {
+		uint32_t emask = 0;
+		for (int j = 0; j < A.d; j++) {
+			// f_j at point k: lo + k (lo + hi), written into the A (j == 0) or B operand
+			if (l < 4) {
+			uint32_t lo[32], hi[32];
+			load_pair<MODE>(A, j, p, l, lo, hi, emask);
+			if (k == 0) {
+			} else if (k == 1) {
+#pragma unroll
+				for (int i = 0; i < 32; i++) lo[i] = hi[i];
+			} else {
+#pragma unroll
+				for (int i = 0; i < 32; i++) hi[i] ^= lo[i];
+#ifdef BN_DEV
+				if (!(A.dbg & 4))
+#endif
+				{
+					if (A.kmax <= 3)  // d <= 3: every k here is 2 or 3 (launch-uniform branch)
+						mul_23(0u - (uint32_t)(k & 1), hi);
+					else
+						mul_small(A.kcol[k], hi, hi);
+				}
+#pragma unroll
+				for (int i = 0; i < 32; i++) lo[i] ^= hi[i];
+			}
+			sst(S, (j == 0 ? 0 : 4) + l, lo);
+			}
+#ifdef BN_DEV
+			if (A.dbg & 2) continue;
+#endif
+			if (j > 0) grp_mul<G, false>(S, nullptr, l, kSkipMid);
+		}
+		wsync();
+		if (l < 4) {
+		uint32_t t[32];
+		sld(t, S, l);
+#ifdef BN_DEV
+		const uint32_t acc = (A.dbg & 8) ? t[0] ^ t[31] : parity_word(t, emask);
+#else
+		const uint32_t acc = parity_word(t, emask);
+#endif
+		if (acc) atomicXor(accL + 4 * k + l, acc);  // LDS atomic
+		}
+	}
+	__syncthreads();
+	if (!A.post) {
+		if (threadIdx.x < 4 * (A.kmax + 1) && accL[threadIdx.x])
+			atomicXor(A.acc + (blockIdx.x % kAccCopies) * kAccStride + threadIdx.x, accL[threadIdx.x]);
+		return;  // sc_post follows
+	}
+	if (gridDim.x == 1) {  // a single workgroup posts its own sums
+		if (threadIdx.x < 4 * (A.kmax + 1)) {
+			A.res[threadIdx.x] = accL[threadIdx.x];
+			if (A.sink) A.sink[threadIdx.x] = accL[threadIdx.x];
+		}
+		if (A.sink && threadIdx.x == 0) A.sink[kResSeq] = (uint32_t)A.skip1 | (A.mode == 2 ? 2u : 0u);
+		__threadfence_system();
+		__syncthreads();
+		if (threadIdx.x == 0) __hip_atomic_store(A.res + kResSeq, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+		return;
+	}
+	// small grids (<= kAccCopies workgroups): workgroup b stores its sums into copy b with plain
+	// stores, the last one to finish XORs the gridDim.x copies and posts the points itself
+	const int nw = 4 * (A.kmax + 1);
+	if (threadIdx.x < nw) A.acc[blockIdx.x * kAccStride + threadIdx.x] = accL[threadIdx.x];
+	uint32_t* last = accL + 4 * (kMaxD + 1);  // (a static __shared__ word cost a workgroup per CU)
+	__syncthreads();
+	if (threadIdx.x == 0)
+		// acq_rel: release orders this workgroup's stores before its count, acquire makes every other
+		// workgroup's stores visible to the last one
+		*last = __hip_atomic_fetch_add(A.acc + kAccCount, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+	__syncthreads();
+	if (!*last) return;
+	__threadfence();
+	uint32_t* red = last + 1;  // 4 (kMaxD + 1) words
+	if (threadIdx.x < nw) red[threadIdx.x] = 0;
+	__syncthreads();
+	// every (copy, word) by one thread, XOR-reduced in LDS
+	for (int i = threadIdx.x; i < (int)gridDim.x * nw; i += kScThreads) {
+		const int b = i / nw, w = i - b * nw;
+		const uint32_t v = __hip_atomic_load(A.acc + b * kAccStride + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if (v) atomicXor(red + w, v);
+	}
+	__syncthreads();
+	if (threadIdx.x < nw) {
+		A.res[threadIdx.x] = red[threadIdx.x];
+		if (A.sink) A.sink[threadIdx.x] = red[threadIdx.x];
+	}
+	if (A.sink && threadIdx.x == 0) A.sink[kResSeq] = (uint32_t)A.skip1 | (A.mode == 2 ? 2u : 0u);
+	__threadfence_system();
+	__syncthreads();
+	if (threadIdx.x == 0) __hip_atomic_store(A.res + kResSeq, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+#ifdef BN_SC_FUSED
+// sc_messages's body as device functions for the fused experiment kernel (sc_fold_msgs). The
+// product kernel above keeps its own copy: the product build is round 5's code.
 // the work-group's point sums in LDS (after the product slots); the accumulator set of the next
 // round is cleared by workgroup 0 (rounds alternate between two sets; the other set was last read
 // back by the previous round's post, ordered before this launch, so no memset is queued per round)
@@ -227,25 +346,6 @@ __device__ __forceinline__ uint32_t* messages_init(const ScArgs& A, uint32_t* ld
 }
 
 // point k of pair p on this group (when `valid`), then the work-group's reduction and posting
-template <int MODE, int G>
-__device__ __forceinline__ void messages_run(const ScArgs& A, uint32_t* lds, uint32_t* accL, size_t p, int k, bool valid);
-
-// One (pair, point k) per group, k fastest: the kmax+1 groups of a pair run side by side, so the
-// pair's columns are read from HBM once and hit in cache for the other points.
-template <int MODE, int G>
-__global__ __launch_bounds__(kScThreads, kScMinWG) void sc_messages(ScArgs A) {
-	extern __shared__ uint32_t lds[];
-	const int qw = threadIdx.x / G;
-	uint32_t* accL = messages_init<G>(A, lds);
-	__syncthreads();
-	const int npts = A.kmax + 1 - A.skip1;
-	const size_t item = (size_t)blockIdx.x * Grp<G>::kGroups + qw;
-	const size_t p = item / npts;
-	const int ki = (int)(item % npts);
-	const int k = (A.skip1 && ki >= 1) ? ki + 1 : ki;
-	messages_run<MODE, G>(A, lds, accL, p, k, p < A.n_pairs);
-}
-
 template <int MODE, int G>
 __device__ __forceinline__ void messages_run(const ScArgs& A, uint32_t* lds, uint32_t* accL, size_t p, int k, bool valid) {
 	const int l = threadIdx.x % G, qw = threadIdx.x / G;
@@ -344,6 +444,8 @@ __device__ __forceinline__ void messages_run(const ScArgs& A, uint32_t* lds, uin
 	__syncthreads();
 	if (threadIdx.x == 0) __hip_atomic_store(A.res + kResSeq, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+
+#endif  // BN_SC_FUSED
 
 // Big grids: a one-wave kernel after sc_messages reduces the copies and posts the points (one
 // counter shared by thousands of workgroups serialised them: 2x the kernel time).
@@ -448,10 +550,13 @@ constexpr int kPairItemsPerWG = kScThreads / 2;
 constexpr size_t kPairMinItems = 384 * (size_t)kPairItemsPerWG;
 __device__ __forceinline__ uint32_t* pair_addr(uint32_t* slot, int w) { return slot + (w >> 6) * kPairRowWords + (w & 63); }
 
+#ifdef BN_SC_FUSED
 // One wave's 32 lane-pair folds. Item q < 32 of the wave folds batch lo_of(q) (nullptr: no item)
-// with the batch A.hb further on, in place. Lane t of the wave moves 16 B of item (t >> 5) + 2 i at
+// with the batch 2 A.n_pairs further on, in place. Lane t of the wave moves 16 B of item (t >> 5) + 2 i at
 // word (4 t) & 127 for i < 16: coalesced 512-B pieces.
-template <class LoOf>
+// (sc_fold_pair keeps its own copy of this body with one base pointer per wave: a per-item pointer
+// here made the product kernel 35 % slower, round 6)
+template <bool MAYBE_NULL, class LoOf>
 __device__ __forceinline__ void fold_pair_wave(const ScArgs& A, uint32_t* slot, int lane, LoOf lo_of) {
 	const int u = lane & 1;
 	uint4 la[16];
@@ -461,8 +566,9 @@ __device__ __forceinline__ void fold_pair_wave(const ScArgs& A, uint32_t* slot, 
 		const uint32_t* lo = lo_of(w >> 7);
 		uint4 b = make_uint4(0, 0, 0, 0);
 		la[i] = b;
-		if (lo) {
-			b = *(const uint4*)(lo + 128 * A.hb + (w & 127));
+		if (!MAYBE_NULL || lo) {
+			b = *(const uint4*)(lo + 256 * A.n_pairs + (w & 127));  // old pair distance 2 hb'
+
 			la[i] = *(const uint4*)(lo + (w & 127));
 		}
 		*(uint4*)pair_addr(slot, w) = make_uint4(la[i].x ^ b.x, la[i].y ^ b.y, la[i].z ^ b.z, la[i].w ^ b.w);
@@ -513,26 +619,85 @@ __device__ __forceinline__ void fold_pair_wave(const ScArgs& A, uint32_t* slot, 
 	for (int i = 0; i < 16; i++) {
 		const int w = 4 * lane + 256 * i;
 		uint32_t* lo = lo_of(w >> 7);
-		if (lo) *(uint4*)(lo + (w & 127)) = *(const uint4*)pair_addr(slot, w);
+		if (!MAYBE_NULL || lo) *(uint4*)(lo + (w & 127)) = *(const uint4*)pair_addr(slot, w);
 	}
 }
 
+#endif  // BN_SC_FUSED
+
 __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_pair(ScArgs A) {
 	extern __shared__ uint32_t lds[];
-	const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+	const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, u = lane & 1;
+	uint32_t* slot = lds + wave * kPairWaveWords;
 	const size_t it0 = (size_t)blockIdx.x * kPairItemsPerWG + 32 * wave;  // the wave's first item
 	if (it0 >= (size_t)A.d * A.n_pairs) return;
 	const int j = (int)(it0 / A.n_pairs);
 	const size_t p0 = it0 % A.n_pairs;
 	uint32_t* lo = A.cols + (size_t)j * A.col_stride + 128 * p0;
-	fold_pair_wave(A, lds + wave * kPairWaveWords, lane, [&](int q) -> uint32_t* { return lo + 128 * q; });
+	const uint32_t* hi = lo + 128 * A.hb;
+	uint4 la[16];
+#pragma unroll
+	for (int i = 0; i < 16; i++) {
+		const int w = 4 * lane + 256 * i;
+		const uint4 b = *(const uint4*)(hi + w);
+		la[i] = *(const uint4*)(lo + w);
+		*(uint4*)pair_addr(slot, w) = make_uint4(la[i].x ^ b.x, la[i].y ^ b.y, la[i].z ^ b.z, la[i].w ^ b.w);
+	}
+	wsync();
+	uint32_t* row = slot + lane * kPairRowWords;
+	uint32_t x[64], t[64];
+#pragma unroll
+	for (int i = 0; i < 64; i += 4) {
+		const uint4 v = *(const uint4*)(row + i);
+		x[i] = v.x, x[i + 1] = v.y, x[i + 2] = v.z, x[i + 3] = v.w;
+	}
+	wsync();  // every row read: the rows take lo
+#pragma unroll
+	for (int i = 0; i < 16; i++) *(uint4*)pair_addr(slot, 4 * lane + 256 * i) = la[i];
+#pragma unroll
+	for (int i = 0; i < 64; i++) t[i] = 0;
+#ifdef BN_DEV
+	if (!(A.dbg & 2))
+#endif
+	bsm6_fma_w2(x, A.r[2], A.r[3], t);  // a_u r1
+	const uint32_t m = 0u - (uint32_t)u;
+	uint32_t o[64];
+	{
+		uint32_t ah[32];
+		bs_alpha<5>(t + 32, ah);
+#pragma unroll
+		for (int i = 0; i < 32; i++) {
+			o[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)t[i], 0xB1, 0xF, 0xF, false) ^ (t[32 + i] & m);
+			o[32 + i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)t[32 + i], 0xB1, 0xF, 0xF, false) ^ ((t[i] ^ ah[i]) & m);
+		}
+	}
+	// (x opaque: the compiler would otherwise share the two products' data-side sums)
+#pragma unroll
+	for (int i = 0; i < 64; i++) asm volatile("" : "+v"(x[i]));
+#ifdef BN_DEV
+	if (!(A.dbg & 2))
+#endif
+	bsm6_fma_w2(x, A.r[0], A.r[1], o);  // + a_u r0
+	wsync();
+#pragma unroll
+	for (int i = 0; i < 64; i += 4) {
+		const uint4 v = *(const uint4*)(row + i);
+		*(uint4*)(row + i) = make_uint4(o[i] ^ v.x, o[i + 1] ^ v.y, o[i + 2] ^ v.z, o[i + 3] ^ v.w);
+	}
+	wsync();
+#pragma unroll
+	for (int i = 0; i < 16; i++) {
+		const int w = 4 * lane + 256 * i;
+		*(uint4*)(lo + w) = *(const uint4*)pair_addr(slot, w);
+	}
 }
 
+#ifdef BN_SC_FUSED
 // Round i's fold fused with round i + 1's messages (the QM31 sibling's
 // qm_fold_messages in GF(2^128) form). A work-group owns P = kGroups / npts consecutive pairs
 // p0 .. p0 + P - 1 of the folded columns (pair distance hb' = A.n_pairs). Phase 1 folds the 2 P d
-// batches they consist of, p' and p' + hb' of every column (old pairs (b, b + 2 hb'), A.hb =
-// 2 hb'), on lane pairs exactly as sc_fold_pair, and writes them in place. Phase 2 runs the
+// batches they consist of, p' and p' + hb' of every column (old pairs (b, b + 2 hb')), on lane
+// pairs as sc_fold_pair, and writes them in place. Phase 2 runs the
 // messages of those P pairs on the quads as sc_messages, reading the batches the work-group has
 // just written (L2) instead of a second kernel reading them back from HBM; one launch per round
 // instead of two. No other work-group reads what this one writes: pair p' reads old batches p',
@@ -548,7 +713,7 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_msgs(ScArgs A) {
 	// phase 1: item v of column j (v < 2 P) folds batch p0 + v (v < P) or hb' + p0 + v - P
 	const int items = 2 * P * A.d;
 	if (32 * wave < items) {
-		fold_pair_wave(A, lds + wave * kPairWaveWords, lane, [&](int q) -> uint32_t* {
+		fold_pair_wave<true>(A, lds + wave * kPairWaveWords, lane, [&](int q) -> uint32_t* {
 			const int it = 32 * wave + q;
 			if (it >= items) return nullptr;
 			const int j = (int)__umulhi((uint32_t)it, A.fm_magic), v = it - j * 2 * P;
@@ -564,6 +729,7 @@ __global__ __launch_bounds__(kScThreads, kScMinWG) void sc_fold_msgs(ScArgs A) {
 	const int k = (A.skip1 && ki >= 1) ? ki + 1 : ki;
 	messages_run<0, 4>(A, lds, accL, p0 + (size_t)lp, k, lp < P && p0 + (size_t)lp < hbn);
 }
+#endif  // BN_SC_FUSED
 // ---------------------------------------------------------------------------------------
 // Round server for the last rounds (at most kServerMaxCur evaluations per column left): ONE
 // resident 768-thread workgroup runs every remaining round by itself. It waits for the host's
@@ -951,13 +1117,17 @@ bool fused_eligible(const bn_sumcheck* sc) {
 }
 
 int launch_fused(bn_sumcheck* sc, const uint32_t* r) {
+#ifndef BN_SC_FUSED
+	(void)sc, (void)r;
+	BN_FAIL(BN_ERR_UNSUPPORTED, "fused fold + messages: experiment builds only (-DBN_SC_FUSED)");
+#else
 	ScArgs A{};
 	A.cols = sc->cols;
 	A.col_stride = sc->col_words;
 	A.d = sc->d;
 	A.mode = 0;
-	A.n_pairs = sc->cur / 64;  // pairs of the folded columns
-	A.hb = 2 * A.n_pairs;      // the fold's pair distance
+	A.n_pairs = sc->cur / 64;  // pairs of the folded columns (the fold's pairs are 2 n_pairs apart)
+	A.hb = A.n_pairs;
 	A.kmax = sc->d;
 	A.skip1 = (sc->have_claim || sc->claim_pending) ? 1 : 0;
 	A.res = sc->d_res;
@@ -987,6 +1157,7 @@ int launch_fused(bn_sumcheck* sc, const uint32_t* r) {
 	sc->par ^= 1;
 	sc->msgs_queued = true;
 	return BN_OK;
+#endif
 }
 
 #ifdef BN_DEV
