@@ -75,6 +75,16 @@ def test_gf128_batched(dev):
     assert np.array_equal(y, O.antt128_batch(xs, log_h, 0))
 
 
+@pytest.mark.parametrize("log_h,r,batch", [(20, 2, 2), (21, 1, 1), (19, 3, 3)])
+def test_gf128_cosets_at_full_launches(log_h, r, batch, dev):
+    # coset bits on launches of many tiles per CU (the LDS-tile passes with their coset twiddle
+    # tables, L = 4 limbs); the smaller (log_h, r) cases above run the small-launch kernels
+    xs = np.stack([O.fill128(300 + 7 * b + r, 400 + b, 1 << log_h) for b in range(batch)])
+    ntt = B.AdditiveNTT(B.AdditiveNTTConf(log_h, r, B.FanPaarTowerField(7)))
+    y = _run_device(ntt, xs.reshape(-1), dev, batch=batch).reshape(batch, -1, 4)
+    assert np.array_equal(y, O.antt128_batch(xs, log_h, r))
+
+
 @pytest.mark.slow
 def test_gf128_north_star_size_limb_md5_and_oracle(ntt_md5, dev):
     # 2^24: limb 0 = the reference's mt19937 stream (MD5-pinned by the reference table),

@@ -47,11 +47,12 @@ def test_sumcheck_transcript_matches_oracle(n, d, transposed, dev):
     sc.close()
 
 
-def test_sumcheck_transcript_quad_path(dev):
-    # n = 18, d = 3: the first rounds are big enough for the throughput kernels (quad products,
-    # the coalesced fold, the separate post kernel); the smaller cases above run the 16-lane ones
-    n, d = 18, 3
-    ev, ch = _case(n, d, 1818)
+@pytest.mark.parametrize("n,d", [(18, 3), (17, 6)])
+def test_sumcheck_transcript_quad_path(n, d, dev):
+    # the first rounds are big enough for the throughput kernels (quad products, the coalesced
+    # fold, the separate post kernel); the smaller cases above run the 16-lane ones. d = 6 takes
+    # the general GF(2^4) k-multiples (mul_small: points up to 6) on the quad path
+    ev, ch = _case(n, d, 1818 if (n, d) == (18, 3) else 1700 + d)
     bs = O.bitslice128(ev)
     want_s, want_p = O.sumcheck_run(bs, n, d, 1, ch)
     sc = B.Sumcheck(n, d, True, bs)
