@@ -5,6 +5,8 @@
 #     library built with 128-thread sumcheck work-groups (lib-t128, -DBN_SC_THREADS=128);
 #  2. VERDICT r5 item 5: 2^24 NTT as 7 + 6 + 11 stages (dev build, BN_BOTTOM_K=11) against
 #     7 + 5 + 12, three alternating pairs, after its parity tests.
+# (setup, in the container: mkdir -p abr/r04 && git archive de2596f | tar -x -C abr/r04 &&
+#  make -C abr/r04/binius-ntt_amd ARCH=gfx950; abr/ is git-ignored)
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"

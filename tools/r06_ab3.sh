@@ -4,6 +4,8 @@
 # product library and on the fused experiment build (lib-fu), then c4 d = 2, 3, 4 of the round-5
 # library (abr/r05, git 979a509, built from its own tree) against the current one, three
 # alternating pairs, and the per-round timelines of both.
+# (setup, in the container: mkdir -p abr/r05 && git archive 979a509 | tar -x -C abr/r05 &&
+#  make -C abr/r05/binius-ntt_amd ARCH=gfx950; abr/ is git-ignored)
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"
