@@ -21,12 +21,60 @@ __global__ __launch_bounds__(256) void k_gf32_mul(const uint32_t* a, const uint3
 		o[i] = (uint32_t)dmul_t<5>(a[i], b[i], tab);
 }
 
-__global__ __launch_bounds__(256) void k_gf128_mul(const uint4* a, const uint4* b, uint4* o, size_t n) {
-	__shared__ uint8_t tab[kGf8LdsBytes];
-	gf8_tables_to_lds(tab);
-	__syncthreads();
-	for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-		o[i] = dmul128_t(a[i], b[i], tab);
+// Elementwise compact GF(2^128) products (bn_gf128_mul_device) on the quad-lane bitsliced product:
+// a wave reads 512 consecutive compact elements of each operand (16-byte coalesced loads) into the
+// LDS slots of its 16 quads, element e of quad q's block into word e of rows c (limb c of a) and
+// 4 + c (of b). Lane l of the quad then turns rows l and 4 + l into limb planes with one 32x32 bit
+// transpose each (bitsliced word i, bit e = bit i of limb l of element e), runs quad_mul, transposes
+// the product's row back, and the wave writes 512 compact products. Per product that is ~96
+// lane-instructions of transposes on top of the quad product's ~435, against ~1360 for the
+// per-lane log/exp Karatsuba of dmul128_t (still the compact repeat microbenchmark, kind 0).
+// Every operand of a wave is in LDS before any product is stored: alias-safe (o == a or o == b).
+__global__ __launch_bounds__(256, 2) void k_gf128_mul(const uint4* a, const uint4* b, uint4* o, size_t n) {
+	extern __shared__ uint32_t lds[];
+	const int t = threadIdx.x & 63, w = threadIdx.x >> 6;
+	const int l = threadIdx.x & 3, qw = threadIdx.x >> 2;
+	const size_t e0 = ((size_t)blockIdx.x * 64 + 16 * w) * 32;  // the wave's first element
+	if (e0 >= n) return;                                        // uniform per wave
+	uint32_t* const wl = lds + 16 * w * quad::kQuadWords;
+	{
+		uint4 ga[8], gb[8];
+#pragma unroll
+		for (int i = 0; i < 8; i++) {
+			const size_t e = e0 + 64 * i + t;
+			ga[i] = e < n ? a[e] : make_uint4(0, 0, 0, 0);
+			gb[i] = e < n ? b[e] : make_uint4(0, 0, 0, 0);
+		}
+#pragma unroll
+		for (int i = 0; i < 8; i++) {
+			const int el = 64 * i + t;
+			uint32_t* const r = wl + (el >> 5) * quad::kQuadWords + (el & 31);
+			r[0] = ga[i].x, r[quad::kRowWords] = ga[i].y, r[2 * quad::kRowWords] = ga[i].z, r[3 * quad::kRowWords] = ga[i].w;
+			r[4 * quad::kRowWords] = gb[i].x, r[5 * quad::kRowWords] = gb[i].y;
+			r[6 * quad::kRowWords] = gb[i].z, r[7 * quad::kRowWords] = gb[i].w;
+		}
+	}
+	quad::wsync();
+	const quad::Slot S{lds + qw * quad::kQuadWords};
+	uint32_t x[32];
+#pragma unroll
+	for (int h = 0; h < 2; h++) {
+		quad::sld(x, S, 4 * h + l);
+		transpose32(x);
+		quad::sst(S, 4 * h + l, x);
+	}
+	quad::quad_mul<false>(S, nullptr, l);  // row l <- (rows 0..3) * (rows 4..7)
+	quad::sld(x, S, l);
+	transpose32(x);
+	quad::sst(S, l, x);
+	quad::wsync();
+#pragma unroll
+	for (int i = 0; i < 8; i++) {
+		const int el = 64 * i + t;
+		const size_t e = e0 + el;
+		const uint32_t* const r = wl + (el >> 5) * quad::kQuadWords + (el & 31);
+		if (e < n) o[e] = make_uint4(r[0], r[quad::kRowWords], r[2 * quad::kRowWords], r[3 * quad::kRowWords]);
+	}
 }
 
 // One thread per 128-word block (transpose_kernel / untranspose_kernel,
@@ -141,14 +189,6 @@ extern "C" int bn_gf32_mul_device(const void* a, const void* b, void* o, size_t 
 	return BN_OK;
 }
 
-extern "C" int bn_gf128_mul_device(const void* a, const void* b, void* o, size_t n, void* stream) {
-	BN_CHECK_ARG(a && b && o, "NULL device pointer");
-	if (!n) return BN_OK;
-	hipLaunchKernelGGL(k_gf128_mul, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, (const uint4*)a,
-					   (const uint4*)b, (uint4*)o, n);
-	BN_HIP(hipGetLastError());
-	return BN_OK;
-}
 
 extern "C" int bn_bitslice_device(void* buf, size_t nblk, int untranspose, void* stream) {
 	BN_CHECK_ARG(buf, "NULL device pointer");
@@ -163,6 +203,20 @@ extern "C" int bn_bitslice_device(void* buf, size_t nblk, int untranspose, void*
 // before every launch (cheap, and correct when the caller switches devices)
 static int quad_kernel_attr(const void* fn) {
 	BN_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)quad_lds_bytes()));
+	return BN_OK;
+}
+
+extern "C" int bn_gf128_mul_device(const void* a, const void* b, void* o, size_t n, void* stream) {
+	BN_CHECK_ARG(a && b && o, "NULL device pointer");
+	if (!n) return BN_OK;
+	int rc = quad_kernel_attr((const void*)k_gf128_mul);
+	if (rc != BN_OK) return rc;
+	// 2048 elements per work-group: 64 quads of 32
+	const size_t grid = (n + 2047) / 2048;
+	BN_CHECK_ARG(grid <= 0x7fffffffu, "too many elements for one launch");
+	hipLaunchKernelGGL(k_gf128_mul, dim3((unsigned)grid), dim3(256), quad_lds_bytes(), (hipStream_t)stream, (const uint4*)a,
+	                   (const uint4*)b, (uint4*)o, n);
+	BN_HIP(hipGetLastError());
 	return BN_OK;
 }
 

@@ -10,10 +10,14 @@
 namespace bn {
 
 // ---- GF(2^8) of the tower by log/exp tables (compact arithmetic leaves) ----
+// lg[0] = 512 (logs of nonzero bytes are 0..254): a product with a zero factor indexes ex at 512 or
+// above, where ex is 0, so a leaf is two log reads, an add and one exp read, with no zero test
+// (the test cost two 64-bit compares, a select and SGPR mask spills per leaf).
 struct Gf8Tables {
-	uint8_t lg[256];
-	uint8_t ex[512];  // ex[i] = g^i for i < 510 (no modular reduction needed for lg[a] + lg[b])
+	uint16_t lg[256];
+	uint8_t ex[1040];  // ex[i] = g^i for i < 510 (no modular reduction for lg[a] + lg[b]), 0 from 510 on
 };
+constexpr int kGf8ExOffset = 512;  // byte offset of ex in the tables
 constexpr Gf8Tables make_gf8_tables() {
 	Gf8Tables t{};
 	uint64_t g = 2;
@@ -27,25 +31,27 @@ constexpr Gf8Tables make_gf8_tables() {
 		if (order == 255) break;
 	}
 	uint64_t x = 1;
-	for (int i = 0; i < 512; i++) {
+	for (int i = 0; i < 510; i++) {
 		t.ex[i] = (uint8_t)x;
-		if (i < 255) t.lg[x] = (uint8_t)i;
+		if (i < 255) t.lg[x] = (uint16_t)i;
 		x = tw_mul(x, g, 3);
 	}
+	t.lg[0] = 512;
 	return t;
 }
 __constant__ constexpr Gf8Tables kGf8 = make_gf8_tables();
-constexpr int kGf8LdsBytes = 768;
+constexpr int kGf8LdsBytes = (int)sizeof(Gf8Tables);
+static_assert(kGf8LdsBytes % 4 == 0 && kGf8LdsBytes == kGf8ExOffset + 1040, "GF(2^8) table layout");
 
-// Copy the tables into (at least 768 bytes of) LDS; the caller synchronises.
+// Copy the tables into (at least kGf8LdsBytes bytes of 4-byte aligned) LDS; the caller synchronises.
 __device__ __forceinline__ void gf8_tables_to_lds(uint8_t* lds_tab) {
 	const uint32_t* src = (const uint32_t*)&kGf8;
 	for (int i = threadIdx.x; i < kGf8LdsBytes / 4; i += blockDim.x) ((uint32_t*)lds_tab)[i] = src[i];
 }
 
 __device__ __forceinline__ uint32_t gf8_mul(uint32_t a, uint32_t b, const uint8_t* tab) {
-	const uint32_t r = tab[256 + tab[a] + tab[b]];
-	return (a && b) ? r : 0u;
+	const uint16_t* lg = (const uint16_t*)tab;
+	return tab[kGf8ExOffset + lg[a] + lg[b]];
 }
 
 // multiply_alpha on the low 2^H bits of a u64 (compile-time height, no recursion at run time)
@@ -61,19 +67,37 @@ __device__ __forceinline__ uint64_t dmul_alpha_u64(uint64_t a) {
 	}
 }
 
-// Compact Karatsuba with GF(2^8) table leaves (H >= 3), values in the low 2^H bits of a u64.
 template <int H>
-__device__ __forceinline__ uint64_t dmul_t(uint64_t a, uint64_t b, const uint8_t* tab) {
+__device__ __forceinline__ uint32_t dmul_alpha(uint32_t a);
+
+// Compact Karatsuba with GF(2^8) table leaves (3 <= H <= 5), values in the low 2^H bits of a u32.
+template <int H>
+__device__ __forceinline__ uint32_t dmul_t32(uint32_t a, uint32_t b, const uint8_t* tab) {
 	if constexpr (H == 3) {
-		return gf8_mul((uint32_t)a, (uint32_t)b, tab);
+		return gf8_mul(a, b, tab);
 	} else {
 		constexpr int half = 1 << (H - 1);
-		constexpr uint64_t m = (half >= 64) ? ~0ull : ((1ull << half) - 1ull);
-		const uint64_t a0 = a & m, a1 = (a >> half) & m, b0 = b & m, b1 = (b >> half) & m;
-		const uint64_t z0 = dmul_t<H - 1>(a0, b0, tab);
-		const uint64_t z2 = dmul_t<H - 1>(a1, b1, tab);
-		const uint64_t z1 = dmul_t<H - 1>(a0 ^ a1, b0 ^ b1, tab) ^ z0 ^ z2;
-		return (z0 ^ z2) | ((z1 ^ dmul_alpha_u64<H - 1>(z2)) << half);
+		constexpr uint32_t m = (1u << half) - 1u;
+		const uint32_t a0 = a & m, a1 = (a >> half) & m, b0 = b & m, b1 = (b >> half) & m;
+		const uint32_t z0 = dmul_t32<H - 1>(a0, b0, tab);
+		const uint32_t z2 = dmul_t32<H - 1>(a1, b1, tab);
+		const uint32_t z1 = dmul_t32<H - 1>(a0 ^ a1, b0 ^ b1, tab) ^ z0 ^ z2;
+		return (z0 ^ z2) | ((z1 ^ dmul_alpha<H - 1>(z2)) << half);
+	}
+}
+
+// The same on a u64 (H <= 6): GF(2^64) splits into u32 halves, so no 64-bit shifts or masks below it.
+template <int H>
+__device__ __forceinline__ uint64_t dmul_t(uint64_t a, uint64_t b, const uint8_t* tab) {
+	if constexpr (H <= 5) {
+		return dmul_t32<H>((uint32_t)a, (uint32_t)b, tab);
+	} else {
+		static_assert(H == 6, "dmul_t: H <= 6 (GF(2^128): dmul128_t)");
+		const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+		const uint32_t z0 = dmul_t32<5>(a0, b0, tab);
+		const uint32_t z2 = dmul_t32<5>(a1, b1, tab);
+		const uint32_t z1 = dmul_t32<5>(a0 ^ a1, b0 ^ b1, tab) ^ z0 ^ z2;
+		return (uint64_t)(z0 ^ z2) | ((uint64_t)(z1 ^ dmul_alpha<5>(z2)) << 32);
 	}
 }
 __device__ __forceinline__ uint4 dmul128_t(uint4 a, uint4 b, const uint8_t* tab) {

@@ -107,3 +107,57 @@ def test_repeat_microbench_kernels_match_oracle(kind, threads, dev):
         for _ in range(iters):
             x = O.mul128(x, to_int(o_c, e))
         assert x == to_int(got, e), e
+
+
+def _mul128_rows(A, Bm):
+    w = lambda x: [(x >> (32 * i)) & 0xFFFFFFFF for i in range(4)]
+    v = lambda r: sum(int(r[i]) << (32 * i) for i in range(4))
+    return np.array([w(O.mul128(v(a), v(b))) for a, b in zip(A, Bm)], dtype=np.uint64).astype(np.uint32)
+
+
+@pytest.mark.parametrize("n", [1, 31, 32, 33, 511, 512, 513, 2047, 2048, 2049, 4100])
+def test_gf128_compact_ragged_sizes(n, dev):
+    """bn_gf128_mul_device runs 512 elements per wave and 2048 per work-group: every ragged tail
+    (partial quad, partial wave, partial work-group) against the oracle, and nothing written past n."""
+    import torch
+    A = _rand(4 * n, 100 + n).reshape(-1, 4)
+    Bm = _rand(4 * n, 200 + n).reshape(-1, 4)
+    ta, tb = _t(A.reshape(-1), dev), _t(Bm.reshape(-1), dev)
+    guard = torch.full((4 * (n + 64),), 0x5A5A5A5A, dtype=torch.int32, device=dev)
+    B.gf128_mul(ta, tb, guard[:4 * n])
+    got = _np(guard)
+    idx = np.arange(0, n, max(1, n // 300))  # every element for small n, a spread for the rest
+    assert np.array_equal(got[:4 * n].reshape(-1, 4)[idx], _mul128_rows(A[idx], Bm[idx]))
+    assert np.all(got[4 * n:] == 0x5A5A5A5A)
+
+
+def test_gf128_compact_alias_safe(dev):
+    n = 3000
+    A = _rand(4 * n, 7).reshape(-1, 4)
+    Bm = _rand(4 * n, 8).reshape(-1, 4)
+    exp = _mul128_rows(A[::97], Bm[::97])
+    ta, tb = _t(A.reshape(-1), dev), _t(Bm.reshape(-1), dev)
+    B.gf128_mul(ta, tb, ta)  # out == a
+    assert np.array_equal(_np(ta).reshape(-1, 4)[::97], exp)
+    ta = _t(A.reshape(-1), dev)
+    B.gf128_mul(ta, tb, tb)  # out == b
+    assert np.array_equal(_np(tb).reshape(-1, 4)[::97], exp)
+
+
+def test_gf128_compact_matches_bitsliced_path_at_size(dev):
+    """2^22 compact products against the bitsliced product (itself oracle- and KAT-checked above)
+    on the same operands: bitslice -> multiply_unrolled<7> -> unbitslice."""
+    import torch
+    n = 1 << 22
+    g = torch.Generator(device="cpu").manual_seed(5)
+    a = torch.randint(-2**31, 2**31, (4 * n,), dtype=torch.int32, generator=g).to(dev)
+    b = torch.randint(-2**31, 2**31, (4 * n,), dtype=torch.int32, generator=g).to(dev)
+    o = torch.empty_like(a)
+    B.gf128_mul(a, b, o)
+    abs_, bbs = a.clone(), b.clone()
+    B.bitslice(abs_)
+    B.bitslice(bbs)
+    B.gf128_mul_bitsliced(abs_, bbs, abs_)
+    B.bitslice(abs_, untranspose=True)
+    torch.cuda.synchronize()
+    assert torch.equal(o, abs_)

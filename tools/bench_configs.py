@@ -81,6 +81,17 @@ def c2(dev, out):
                                      "HBM-resident 128-word blocks", "value": prods / (ms * 1e-3), "unit": "products/s",
          "ms": ms, "hbm_gbps_algorithmic": 3 * 512.0 * nblk / (ms * 1e-3) / 1e9, "kernel": "bn::k_gf128_mul_bs"})
     del a, b, o
+    # the compact entry on HBM-resident operands: dst = a * b over 2^25 compact elements
+    # (tower_height_7_mul semantics; 48 B of HBM traffic per product)
+    n = 1 << 25
+    a = torch.randint(-2**31, 2**31, (4 * n,), dtype=torch.int32, device=dev)
+    b = torch.randint(-2**31, 2**31, (4 * n,), dtype=torch.int32, device=dev)
+    o = torch.empty_like(a)
+    ms = ev_time(lambda: B.gf128_mul(a, b, o, stream=st), 5, st)
+    out({"config": "c2", "workload": "GF(2^128) compact products through bn_gf128_mul_device, 2^25 HBM-resident "
+                                     "elements", "value": n / (ms * 1e-3), "unit": "products/s", "ms": ms,
+         "hbm_gbps_algorithmic": 48.0 * n / (ms * 1e-3) / 1e9, "kernel": "bn::k_gf128_mul"})
+    del a, b, o
 
 
 def ntt_line(dev, out, cfg, log_h, batch):
