@@ -837,7 +837,7 @@ static std::vector<BsPass> plan_passes(const bn_antt_plan* plan) {
 			while (g < kBlkBits && hi - g - 1 >= bottom_k && gf8_stage(hi - g - 1)) g++;
 			const int min_first = (hi - bottom_k) - (remaining_up - 1) * kBlkBits;  // the rest must still fit
 			if (g > k && g >= min_first) k = g;
-		}
+		BN_DEV_FIRST_K(k, min_first); }  // development build: BN_FIRST_K=k overrides the first pass's stage count
 #endif
 		passes.push_back(make(hi - k, k, false));
 		hi -= k;

@@ -37,3 +37,15 @@ void clear_error();
 	do {                                             \
 		if (!(cond)) BN_FAIL(BN_ERR_INVALID, __VA_ARGS__); \
 	} while (0)
+
+// Development build only (make BN_DEV=1): BN_FIRST_K=k gives the first upper pass of the bitsliced
+// plan k stages (antt_bs.hip plan_passes; round-6 A/B of 6 + 6 + 12, tools/r06_ab4.sh), bounded
+// below by what the later passes need. A no-op in the product build.
+#ifdef BN_DEV
+#define BN_DEV_FIRST_K(k, lo)                                                        \
+	do {                                                                             \
+		if (const char* e_ = getenv("BN_FIRST_K")) (k) = std::max((lo), std::min(kBlkBits, atoi(e_))); \
+	} while (0)
+#else
+#define BN_DEV_FIRST_K(k, lo) ((void)0)
+#endif
