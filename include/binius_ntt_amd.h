@@ -105,7 +105,9 @@ int bn_antt_pass_kernel_name(bn_antt_plan* plan, int pass, char* buf, size_t cap
  * Binary tower field arithmetic (src/ulvt/finite_fields/)
  * ------------------------------------------------------------------------------------ */
 /* Elementwise GF(2^128) product of compact vectors, n elements, device pointers.
- * Semantics of tower_height_7_mul (src/ulvt/sumcheck/test/utils/tower_7_mul.cu:4-20). */
+ * Semantics of tower_height_7_mul (src/ulvt/sumcheck/test/utils/tower_7_mul.cu:4-20). Any n;
+ * alias-safe (d_out == d_a or d_out == d_b). Runs on the bitsliced quad-lane product behind
+ * in-LDS bit transposes (78 KB of dynamic LDS per work-group). */
 int bn_gf128_mul_device(const void* d_a, const void* d_b, void* d_out, size_t n, void* stream);
 /* Same on bitsliced 128-word blocks: multiply_unrolled<7> (circuit_generator/unrolled/
  * binary_tower_unrolled7.cu), n_blocks blocks of 32 products each. Alias-safe (d_out == d_a). */
