@@ -161,3 +161,21 @@ def test_gf128_compact_matches_bitsliced_path_at_size(dev):
     B.bitslice(abs_, untranspose=True)
     torch.cuda.synchronize()
     assert torch.equal(o, abs_)
+
+
+@pytest.mark.parametrize("n", [1, 255, 4097])
+def test_gf32_random_and_zero_operands(n, dev):
+    """bn_gf32_mul_device on random words with zero bytes planted (the GF(2^8) leaves index the
+    exp table at log(0) = 512 and above, where it holds 0), against the oracle's tower product."""
+    import torch
+    a = _rand(n, 300 + n)
+    b = _rand(n, 400 + n)
+    a[::3] &= 0xFFFF00FF  # a zero byte in a leaf operand
+    b[::5] &= 0x00FFFFFF
+    a[::7] = 0
+    b[1::11] = 0
+    ta, tb = _t(a, dev), _t(b, dev)
+    o = torch.empty_like(ta)
+    B.gf32_mul(ta, tb, o)
+    exp = np.array([O.mul(int(x), int(y), 5) for x, y in zip(a, b)], dtype=np.uint64).astype(np.uint32)
+    assert np.array_equal(_np(o), exp)
