@@ -38,6 +38,8 @@
 #include "quad_mul.hpp"
 #include "tower.hpp"
 
+int bitslice_launch(const void* src, void* dst, size_t nblk, int untranspose, hipStream_t st);  // field.hip
+
 namespace bn {
 namespace {
 
@@ -1448,10 +1450,21 @@ extern "C" int bn_sumcheck_create_device(int device, int num_vars, int d, int tr
 			return rc;
 		}
 		hipError_t e = hipSuccess;
-		if (col_words != in_words) e = hipMemsetAsync(sc->cols, 0, sizeof(uint32_t) * col_words * (size_t)d, sc->stream);
-		for (int j = 0; j < d && e == hipSuccess; j++)
-			e = hipMemcpyAsync(sc->cols + (size_t)j * col_words, (const uint32_t*)d_evals + (size_t)j * in_words,
-							   sizeof(uint32_t) * in_words, hipMemcpyDeviceToDevice, sc->stream);
+		if (!transposed && col_words == in_words) {
+			// compact columns of whole blocks: bit-transposed straight from the caller's buffer into the
+			// prover's storage (one pass over HBM instead of a copy and an in-place transpose)
+			rc = bitslice_launch(d_evals, sc->cols, col_words / 128 * (size_t)d, 0, sc->stream);
+			if (rc != BN_OK) {
+				sc_free(sc);
+				return rc;
+			}
+			transposed = 1;
+		} else {
+			if (col_words != in_words) e = hipMemsetAsync(sc->cols, 0, sizeof(uint32_t) * col_words * (size_t)d, sc->stream);
+			for (int j = 0; j < d && e == hipSuccess; j++)
+				e = hipMemcpyAsync(sc->cols + (size_t)j * col_words, (const uint32_t*)d_evals + (size_t)j * in_words,
+								   sizeof(uint32_t) * in_words, hipMemcpyDeviceToDevice, sc->stream);
+		}
 		if (e == hipSuccess && take) e = hipStreamSynchronize(sc->stream);
 		if (e == hipSuccess && take) e = hipFree(d_evals);
 		if (e != hipSuccess) {

@@ -66,6 +66,41 @@ def test_bitslice_roundtrip_matches_oracle(dev):
     assert np.array_equal(_np(t), x)
 
 
+@pytest.mark.parametrize("nblk", [1, 15, 16, 17, 63, 64, 65, 1000])
+def test_bitslice_sizes_both_directions(nblk, dev):
+    """bn_bitslice_device runs 16 blocks per wave and 64 per work-group: every ragged tail, in both
+    directions, against BitsliceUtils (the oracle), and nothing written past the last block."""
+    import torch
+    x = _rand(128 * nblk, 600 + nblk)
+    buf = torch.full((128 * (nblk + 16),), 0x3C3C3C3C, dtype=torch.int32, device=dev)
+    buf[:128 * nblk] = _t(x, dev)
+    B.bitslice(buf[:128 * nblk])
+    got = _np(buf)
+    assert np.array_equal(got[:128 * nblk], O.bitslice128(x))
+    assert np.all(got[128 * nblk:] == 0x3C3C3C3C)
+    y = _rand(128 * nblk, 700 + nblk)
+    buf[:128 * nblk] = _t(y, dev)
+    B.bitslice(buf[:128 * nblk], untranspose=True)
+    got = _np(buf)
+    assert np.array_equal(got[:128 * nblk], O.unbitslice128(y))
+    assert np.all(got[128 * nblk:] == 0x3C3C3C3C)
+
+
+def test_bitslice_round_trip_at_size(dev):
+    """2^20 blocks (512 MiB): untranspose(transpose(x)) == x, and a sampled block against the oracle."""
+    import torch
+    g = torch.Generator(device="cpu").manual_seed(9)
+    x = torch.randint(-2**31, 2**31, (128 << 20,), dtype=torch.int32, generator=g).to(dev)
+    y = x.clone()
+    B.bitslice(y)
+    blk = 777777
+    want = O.bitslice128(x[128 * blk:128 * (blk + 1)].cpu().numpy().view(np.uint32))
+    assert np.array_equal(_np(y[128 * blk:128 * (blk + 1)]), want)
+    B.bitslice(y, untranspose=True)
+    torch.cuda.synchronize()
+    assert torch.equal(x, y)
+
+
 def test_bitsliced_gf128_mul_kat_and_random(field_kats, dev):
     import torch
     # reference KAT block (test_fanpaartower.cu:199-273) padded with random elements

@@ -470,3 +470,24 @@ def test_big_round_abandoned_prover(dev):
     got_s, got_p = _transcript(sc, n, ch)
     sc.close()
     assert np.array_equal(got_s, want_s) and np.array_equal(got_p, want_p)
+
+
+@pytest.mark.parametrize("n,d", [(4, 2), (5, 3), (6, 2), (10, 4), (16, 3)])
+def test_device_compact_input_matches_host_input(n, d, dev):
+    """A prover built from compact device columns transposes them straight into its storage
+    (bn_sumcheck_create_device: one bitslice pass from the caller's buffer; below one whole block,
+    n < 5, a padded copy and an in-place transpose); its transcript equals the host-built prover's,
+    and the caller's buffer is left untouched."""
+    import torch
+    host = _rand(4 * (1 << n) * d, 5150 + n)
+    ev = torch.from_numpy(host.view(np.int32)).to(dev)
+    ch = _rand(4 * n, 5151 + n).reshape(n, 4)
+    sc = B.Sumcheck(n, d, False, ev)
+    got_s, got_p = _transcript(sc, n, ch)
+    sc.close()
+    ref = B.Sumcheck(n, d, False, host)
+    want_s, want_p = _transcript(ref, n, ch)
+    ref.close()
+    assert np.array_equal(got_s, want_s) and np.array_equal(got_p, want_p)
+    torch.cuda.synchronize()
+    assert np.array_equal(ev.cpu().numpy().view(np.uint32), host)
